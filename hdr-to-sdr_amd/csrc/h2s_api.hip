@@ -1,0 +1,544 @@
+// h2s_api.hip — the C-ABI (include/h2s.h): contexts, parameter resolution,
+// LUT upload, frame validation, host staging and kernel timing.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/h2s.h"
+#include "h2s_device.h"
+
+namespace h2s {
+hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
+hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
+}  // namespace h2s
+
+using h2s::KParams;
+
+namespace {
+thread_local std::string g_err;  // errors with no context
+constexpr int kEvRing = 256;
+}  // namespace
+
+struct h2s_ctx {
+  int device = 0;
+  h2s_params params{};
+  bool params_set = false;
+  KParams k{};  // resolved constants (pointers filled per call)
+  float4* d_lut = nullptr;
+  int lut_n = 0;
+  uint16_t* d_eq = nullptr;
+  void* d_stage = nullptr;
+  size_t stage_bytes = 0;
+  std::string err;
+  bool timing = false;
+  hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
+  long long ev_count = 0;  // launches recorded since reset
+};
+
+namespace {
+
+int fail(h2s_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  else g_err = msg;
+  return code;
+}
+
+int hip_fail(h2s_ctx* c, hipError_t e, const char* what) {
+  return fail(c, H2S_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+  }
+};
+
+// ---- parameter resolution (mirrors vf_tonemap init/filter_frame, zimg,
+// vf_eq create_lut; the CPU statement is oracle/h2s_oracle.c resolve()) ----
+float hable_h(float in) {
+  const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
+  return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
+}
+
+double pq_encode_d(double y) {
+  const double m1 = 0.1593017578125, m2 = 78.84375, c1 = 0.8359375, c2 = 18.8515625, c3 = 18.6875;
+  double ym = pow(fmax(y, 0.0), m1);
+  return pow((c1 + c2 * ym) / (1.0 + c3 * ym), m2);
+}
+
+int validate_params(h2s_ctx* c, const h2s_params* p) {
+  if (p->transfer_in != H2S_TRC_PQ && p->transfer_in != H2S_TRC_HLG)
+    return fail(c, H2S_E_INVALID_ARG, "transfer_in must be PQ or HLG");
+  if (p->bits_in != 10 && p->bits_in != 12)
+    return fail(c, H2S_E_UNSUPPORTED, "bits_in must be 10 or 12 (yuv420p10le / yuv420p12le)");
+  if (p->bits_out != 8 && p->bits_out != 10 && p->bits_out != 12)
+    return fail(c, H2S_E_UNSUPPORTED, "bits_out must be 8, 10 or 12");
+  if (p->tonemap < H2S_TM_NONE || p->tonemap > H2S_TM_BT2390)
+    return fail(c, H2S_E_INVALID_ARG, "unknown tonemap operator");
+  if (p->mode != H2S_MODE_COMPAT8 && p->mode != H2S_MODE_NATIVE)
+    return fail(c, H2S_E_INVALID_ARG, "mode must be COMPAT8 or NATIVE");
+  if (p->desat_luma < 0 || p->desat_luma > 2) return fail(c, H2S_E_INVALID_ARG, "unknown desat_luma");
+  if (!(p->gamma > 0) || !isfinite(p->gamma)) return fail(c, H2S_E_INVALID_ARG, "gamma must be > 0");
+  if (!(p->npl > 0) || !isfinite(p->npl)) return fail(c, H2S_E_INVALID_ARG, "npl must be > 0");
+  if (!(p->desat >= 0)) return fail(c, H2S_E_INVALID_ARG, "desat must be >= 0");
+  return 0;
+}
+
+void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
+  memset(k, 0, sizeof(*k));
+  // S1 zimg: depth conversion (limited range), BT.2020-NCL matrix, scale
+  const int sh = p->bits_in - 8;
+  k->y_scale = (float)(1.0 / (219 << sh));
+  k->y_off = (float)(-(double)(16 << sh) / (219 << sh));
+  k->c_scale = (float)(1.0 / (224 << sh));
+  k->c_off = (float)(-(double)(128 << sh) / (224 << sh));
+  const double kr = 0.2627, kb = 0.0593, kg = 1.0 - kr - kb;
+  k->m_rcr = (float)(2.0 * (1.0 - kr));
+  k->m_gcb = (float)(-2.0 * kb * (1.0 - kb) / kg);
+  k->m_gcr = (float)(-2.0 * kr * (1.0 - kr) / kg);
+  k->m_bcb = (float)(2.0 * (1.0 - kb));
+  k->transfer = p->transfer_in;
+  k->lin_scale = (float)((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl);
+
+  // S2 vf_tonemap init defaults
+  double param = p->tm_param;
+  switch (p->tonemap) {
+    case H2S_TM_GAMMA:
+      if (isnan(param)) param = 1.8;
+      break;
+    case H2S_TM_REINHARD:
+      if (!isnan(param)) param = (1.0 - param) / param;
+      break;
+    case H2S_TM_MOBIUS:
+      if (isnan(param)) param = 0.3;
+      break;
+  }
+  if (isnan(param)) param = 1.0;
+  // ff_determine_signal_peak; trc at tonemap's input is linear -> 10.0
+  double peak = p->peak;
+  if (!(peak > 0)) {
+    peak = 0;
+    if (p->maxcll > 0) peak = p->maxcll / 100.0;
+    if (!(peak > 0) && p->mastering_max > 0) peak = p->mastering_max / 100.0;
+    if (!(peak > 0)) peak = 10.0;
+  }
+  k->tonemap = p->tonemap;
+  k->desat_on = p->desat > 0 ? 1 : 0;
+  k->desat = (float)p->desat;
+  switch (p->desat_luma) {
+    case H2S_DESAT_LUMA_BT2020: k->lr = 0.2627f, k->lg = 0.6780f, k->lb = 0.0593f; break;
+    case H2S_DESAT_LUMA_BT709: k->lr = 0.2126f, k->lg = 0.7152f, k->lb = 0.0722f; break;
+    default: k->lr = 1.0f, k->lg = 1.0f, k->lb = 1.0f;
+  }
+  k->lin_k = (float)(param / peak);
+  k->gam_inv_peak = (float)(1.0 / peak);
+  k->gam_inv_param = (float)(1.0 / param);
+  k->gam_low_k = (float)(pow(0.05 / peak, 1.0 / param) / 0.05);
+  k->clip_k = (float)param;
+  k->hable_peak_inv = 1.0f / hable_h((float)peak);
+  k->rein_p = (float)param;
+  k->rein_k = (float)((peak + param) / peak);
+  {
+    const float j = (float)param;
+    const float a = (float)(-j * j * (peak - 1.0f) / (j * j - 2.0f * j + peak));
+    const float b = (float)((j * j - 2.0f * j * peak + peak) / fmax(peak - 1.0f, 1e-6));
+    k->mob_j = j, k->mob_a = a, k->mob_b = b;
+    k->mob_k = (b * b + 2.0f * b * j + j * j) / (b - a);
+  }
+  {
+    const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
+    const double ml = (pq_encode_d(p->npl / 10000.0) - smin) / (smax - smin);
+    const double ks = 1.5 * ml - 0.5;
+    k->b_srcmin = (float)smin;
+    k->b_range = (float)(smax - smin);
+    k->b_inv_range = (float)(1.0 / (smax - smin));
+    k->b_ks = (float)ks;
+    k->b_inv_1mks = (float)(1.0 / (1.0 - ks));
+    k->b_maxlum = (float)ml;
+  }
+  k->npl_1e4 = (float)(p->npl / 10000.0);
+  k->e4_npl = (float)(10000.0 / p->npl);
+  // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
+  const double m[9] = {1.6604910021, -0.5876411388, -0.0728498633, -0.1245504745, 1.1328998971,
+                       -0.0083494226, -0.0181507634, -0.1005788980, 1.1187296614};
+  for (int i = 0; i < 9; i++) k->m709[i] = (float)m[i];
+  k->lut_enabled = p->lut_enabled ? 1 : 0;
+  // S6 BT.709 limited-range Y'CbCr rows
+  const double r709 = 0.2126, g709 = 0.7152, b709 = 0.0722;
+  k->k709[0] = (float)r709, k->k709[1] = (float)g709, k->k709[2] = (float)b709;
+  k->kcb[0] = (float)(-r709 / 1.8556), k->kcb[1] = (float)(-g709 / 1.8556), k->kcb[2] = (float)(0.9278 / 1.8556);
+  k->kcr[0] = (float)(0.7874 / 1.5748), k->kcr[1] = (float)(-g709 / 1.5748), k->kcr[2] = (float)(-b709 / 1.5748);
+  const int q = p->mode == H2S_MODE_NATIVE ? p->bits_out : 8;
+  k->qmax = (1 << q) - 1;
+  k->qscale = (float)(1 << (q - 8));
+  k->shift_out = p->mode == H2S_MODE_NATIVE ? 0 : p->bits_out - 8;
+  // S7 vf_eq create_lut, generalised to 2^q entries
+  const int qn = 1 << q;
+  eq->assign(qn, 0);
+  bool ident = true;
+  const double g = 1.0 / p->gamma;
+  for (int i = 0; i < qn; i++) {
+    double v = i / (double)(qn - 1);
+    uint16_t o;
+    if (v <= 0.0) {
+      o = 0;
+    } else {
+      v = pow(v, g);
+      o = v >= 1.0 ? (uint16_t)(qn - 1) : (uint16_t)(int)((double)qn * v);
+    }
+    (*eq)[i] = o;
+    if (o != i) ident = false;
+  }
+  k->eq_identity = ident ? 1 : 0;
+}
+
+bool aligned(const void* p, long long a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
+
+int check_frames(h2s_ctx* c, const h2s_frames* f, int bits, const char* which) {
+  if (!f) return fail(c, H2S_E_INVALID_ARG, std::string(which) + " frames is NULL");
+  if (f->width <= 0 || f->height <= 0) return fail(c, H2S_E_INVALID_ARG, std::string(which) + ": empty frame");
+  if ((f->width & 1) || (f->height & 1))
+    return fail(c, H2S_E_UNSUPPORTED, std::string(which) + ": 4:2:0 frames need even width and height");
+  if (f->bits != bits)
+    return fail(c, H2S_E_INVALID_ARG,
+                std::string(which) + ": bits " + std::to_string(f->bits) + " != params " + std::to_string(bits));
+  if (f->location != H2S_LOC_DEVICE && f->location != H2S_LOC_HOST)
+    return fail(c, H2S_E_INVALID_ARG, std::string(which) + ": bad location");
+  const int bps = bits == 8 ? 1 : 2;
+  const long long rowb[3] = {(long long)f->width * bps, (long long)f->width / 2 * bps, (long long)f->width / 2 * bps};
+  for (int p = 0; p < 3; p++) {
+    if (!f->data[p]) return fail(c, H2S_E_INVALID_ARG, std::string(which) + ": NULL plane");
+    if (f->linesize[p] < rowb[p])
+      return fail(c, H2S_E_INVALID_ARG, std::string(which) + ": linesize smaller than a row");
+    if (bps == 2 && ((f->linesize[p] & 1) || !aligned(f->data[p], 2)))
+      return fail(c, H2S_E_INVALID_ARG, std::string(which) + ": 16-bit planes must be 2-byte aligned");
+  }
+  return 0;
+}
+
+// vector path needs 16-B luma / 8-B chroma alignment of every row start
+bool vec_ok(const h2s_frames* f, bool out8) {
+  const long long ay = out8 ? 8 : 16, ac = out8 ? 4 : 8;
+  const long long a[3] = {ay, ac, ac};
+  for (int p = 0; p < 3; p++)
+    if (!aligned(f->data[p], a[p]) || f->linesize[p] % a[p] || f->frame_pitch[p] % a[p]) return false;
+  return true;
+}
+
+size_t frame_bytes(const h2s_frames* f) {
+  const size_t bps = f->bits == 8 ? 1 : 2;
+  return (size_t)f->width * f->height * bps * 3 / 2;
+}
+
+// tight device copy descriptor laid out in `base`
+h2s_frames tight(const h2s_frames* f, void* base) {
+  h2s_frames t = *f;
+  const long long bps = f->bits == 8 ? 1 : 2;
+  const long long ysz = (long long)f->width * f->height * bps, csz = ysz / 4;
+  const long long fb = ysz + 2 * csz;
+  t.data[0] = base;
+  t.data[1] = (uint8_t*)base + ysz;
+  t.data[2] = (uint8_t*)base + ysz + csz;
+  t.linesize[0] = f->width * bps;
+  t.linesize[1] = t.linesize[2] = f->width / 2 * bps;
+  t.frame_pitch[0] = t.frame_pitch[1] = t.frame_pitch[2] = fb;
+  t.location = H2S_LOC_DEVICE;
+  return t;
+}
+
+hipError_t copy_frames(const h2s_frames* dst, const h2s_frames* src, int nframes, hipStream_t s) {
+  const long long bps = src->bits == 8 ? 1 : 2;
+  for (int fr = 0; fr < nframes; fr++)
+    for (int p = 0; p < 3; p++) {
+      const long long w = (p ? src->width / 2 : src->width) * bps, h = p ? src->height / 2 : src->height;
+      hipError_t e = hipMemcpy2DAsync((uint8_t*)dst->data[p] + fr * dst->frame_pitch[p], dst->linesize[p],
+                                      (const uint8_t*)src->data[p] + fr * src->frame_pitch[p], src->linesize[p], w,
+                                      h, hipMemcpyDefault, s);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+void fill_geometry(KParams* k, const h2s_frames* in, const h2s_frames* out, int nframes) {
+  k->W = in->width;
+  k->H = in->height;
+  k->cw = in->width / 2;
+  k->ch = in->height / 2;
+  k->ngx = (k->cw + 3) / 4;
+  k->nframes = nframes;
+  k->total = (long long)nframes * k->ch * k->ngx;
+  for (int p = 0; p < 3; p++) {
+    k->in[p] = (const uint8_t*)in->data[p];
+    k->in_ls[p] = in->linesize[p];
+    k->in_fp[p] = in->frame_pitch[p];
+    if (out) {
+      k->out[p] = (uint8_t*)out->data[p];
+      k->out_ls[p] = out->linesize[p];
+      k->out_fp[p] = out->frame_pitch[p];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int h2s_abi_version(void) { return H2S_ABI_VERSION; }
+
+const char* h2s_last_error(const h2s_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+void h2s_params_default(h2s_params* p) {
+  if (!p) return;
+  memset(p, 0, sizeof(*p));
+  // FFMPEG_CONVERT_FILTER defaults (src/utils.py:38-42) with the settings
+  // defaults (src/settings.py:10-26: gamma 1.0, tonemapper Mobius) and the
+  // GUI's 10-bit output for <=10-bit sources (src/gui.py:1009-1021).
+  p->transfer_in = H2S_TRC_PQ;
+  p->bits_in = 10;
+  p->bits_out = 10;
+  p->tonemap = H2S_TM_MOBIUS;
+  p->tm_param = NAN;
+  p->desat = 2.0;
+  p->peak = 0.0;
+  p->npl = 100.0;
+  p->gamma = 1.0;
+  p->lut_enabled = 1;
+  p->mode = H2S_MODE_COMPAT8;
+  p->desat_luma = H2S_DESAT_LUMA_RGB;
+}
+
+int h2s_create(int device, h2s_ctx** out) {
+  if (!out) return fail(nullptr, H2S_E_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return fail(nullptr, H2S_E_HIP, "no HIP device available");
+  if (device < 0 || device >= n) return fail(nullptr, H2S_E_INVALID_ARG, "device ordinal out of range");
+  h2s_ctx* c = new (std::nothrow) h2s_ctx();
+  if (!c) return fail(nullptr, H2S_E_OOM, "context allocation failed");
+  c->device = device;
+  h2s_params_default(&c->params);
+  *out = c;
+  return 0;
+}
+
+void h2s_destroy(h2s_ctx* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  hipDeviceSynchronize();
+  if (c->d_lut) hipFree(c->d_lut);
+  if (c->d_eq) hipFree(c->d_eq);
+  if (c->d_stage) hipFree(c->d_stage);
+  for (int i = 0; i < kEvRing; i++) {
+    if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
+    if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
+  }
+  delete c;
+}
+
+int h2s_set_lut(h2s_ctx* c, const float* rgb, int n) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (!rgb || n < 2 || n > 256) return fail(c, H2S_E_INVALID_ARG, "LUT size must be in [2, 256]");
+  DeviceGuard g(c->device);
+  const size_t cnt = (size_t)n * n * n;
+  std::vector<float4> host(cnt);
+  for (size_t i = 0; i < cnt; i++) host[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.0f);
+  if (c->d_lut && c->lut_n != n) {
+    hipFree(c->d_lut);
+    c->d_lut = nullptr;
+  }
+  if (!c->d_lut) {
+    hipError_t e = hipMalloc((void**)&c->d_lut, cnt * sizeof(float4));
+    if (e != hipSuccess) {
+      c->d_lut = nullptr;
+      return fail(c, H2S_E_OOM, "LUT device allocation failed");
+    }
+  }
+  hipError_t e = hipMemcpy(c->d_lut, host.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(c, e, "LUT upload");
+  c->lut_n = n;
+  return 0;
+}
+
+int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (!p) return fail(c, H2S_E_INVALID_ARG, "params is NULL");
+  int rc = validate_params(c, p);
+  if (rc) return rc;
+  DeviceGuard g(c->device);
+  std::vector<uint16_t> eq;
+  KParams k;
+  resolve(p, &k, &eq);
+  if (!c->d_eq) {
+    hipError_t e = hipMalloc((void**)&c->d_eq, 4096 * sizeof(uint16_t));
+    if (e != hipSuccess) {
+      c->d_eq = nullptr;
+      return fail(c, H2S_E_OOM, "eq table allocation failed");
+    }
+  }
+  hipError_t e = hipMemcpy(c->d_eq, eq.data(), eq.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(c, e, "eq table upload");
+  c->params = *p;
+  c->k = k;
+  c->params_set = true;
+  return 0;
+}
+
+static int prepare(h2s_ctx* c, KParams* k) {
+  if (!c->params_set) return fail(c, H2S_E_INVALID_ARG, "h2s_set_params was not called");
+  if (c->params.lut_enabled && !c->d_lut)
+    return fail(c, H2S_E_LUT_MISSING, "lut_enabled but no LUT loaded (h2s_set_lut)");
+  *k = c->k;
+  k->lut = c->d_lut;
+  k->lut_n = c->lut_n;
+  k->lut_sg = c->lut_n;
+  k->lut_sb = c->lut_n * c->lut_n;
+  k->lut_max = (float)(c->lut_n - 1);
+  k->eq_lut = c->d_eq;
+  return 0;
+}
+
+int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nframes, void* hip_stream) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (nframes < 0) return fail(c, H2S_E_INVALID_ARG, "nframes < 0");
+  KParams k;
+  int rc = prepare(c, &k);
+  if (rc) return rc;
+  if ((rc = check_frames(c, in, c->params.bits_in, "input"))) return rc;
+  if ((rc = check_frames(c, out, c->params.bits_out, "output"))) return rc;
+  if (in->width != out->width || in->height != out->height)
+    return fail(c, H2S_E_INVALID_ARG, "input and output frame sizes differ");
+  if (nframes == 0) return 0;
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)hip_stream;
+  const bool out8 = c->params.bits_out == 8;
+
+  h2s_frames din = *in, dout = *out;
+  const bool host_in = in->location == H2S_LOC_HOST, host_out = out->location == H2S_LOC_HOST;
+  if (host_in || host_out) {
+    const size_t ib = host_in ? frame_bytes(in) * nframes : 0, ob = host_out ? frame_bytes(out) * nframes : 0;
+    const size_t need = ((ib + 255) / 256) * 256 + ob;
+    if (need > c->stage_bytes) {
+      if (c->d_stage) hipFree(c->d_stage);
+      c->d_stage = nullptr;
+      c->stage_bytes = 0;
+      hipError_t e = hipMalloc(&c->d_stage, need);
+      if (e != hipSuccess) {
+        c->d_stage = nullptr;
+        return fail(c, H2S_E_OOM, "staging allocation failed");
+      }
+      c->stage_bytes = need;
+    }
+    if (host_in) {
+      din = tight(in, c->d_stage);
+      hipError_t e = copy_frames(&din, in, nframes, s);
+      if (e != hipSuccess) return hip_fail(c, e, "host->device copy");
+    }
+    if (host_out) dout = tight(out, (uint8_t*)c->d_stage + ((ib + 255) / 256) * 256);
+  }
+  fill_geometry(&k, &din, &dout, nframes);
+  const bool vec = vec_ok(&din, false) && vec_ok(&dout, out8);
+  const int slot = (int)(c->ev_count % kEvRing);
+  if (c->timing) {
+    if (!c->ev0[slot]) {
+      hipEventCreate(&c->ev0[slot]);
+      hipEventCreate(&c->ev1[slot]);
+    }
+    hipEventRecord(c->ev0[slot], s);
+  }
+  hipError_t e = h2s::launch_process(k, vec, out8, s);
+  if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+  if (c->timing) {
+    hipEventRecord(c->ev1[slot], s);
+    c->ev_count++;
+  }
+  if (host_out) {
+    e = copy_frames(out, &dout, nframes, s);
+    if (e != hipSuccess) return hip_fail(c, e, "device->host copy");
+  }
+  if (host_in || host_out) {
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(c, e, "stream synchronize");
+  }
+  return 0;
+}
+
+int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb, int out_location,
+                    void* hip_stream) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (stage < H2S_STAGE_LINEAR || stage > H2S_STAGE_LUT) return fail(c, H2S_E_INVALID_ARG, "bad stage");
+  if (!out_rgb) return fail(c, H2S_E_INVALID_ARG, "out_rgb is NULL");
+  KParams k;
+  int rc = prepare(c, &k);
+  if (rc) return rc;
+  if ((rc = check_frames(c, in, c->params.bits_in, "input"))) return rc;
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)hip_stream;
+  const size_t npx = (size_t)in->width * in->height, ob = npx * 3 * sizeof(float);
+  void* din_mem = nullptr;
+  float* dout = out_rgb;
+  h2s_frames din = *in;
+  hipError_t e;
+  if (in->location == H2S_LOC_HOST) {
+    if ((e = hipMalloc(&din_mem, frame_bytes(in))) != hipSuccess) return fail(c, H2S_E_OOM, "debug alloc");
+    din = tight(in, din_mem);
+    if ((e = copy_frames(&din, in, 1, s)) != hipSuccess) {
+      hipFree(din_mem);
+      return hip_fail(c, e, "debug copy");
+    }
+  }
+  if (out_location == H2S_LOC_HOST) {
+    if ((e = hipMalloc((void**)&dout, ob)) != hipSuccess) {
+      if (din_mem) hipFree(din_mem);
+      return fail(c, H2S_E_OOM, "debug alloc");
+    }
+  }
+  fill_geometry(&k, &din, nullptr, 1);
+  e = h2s::launch_debug(k, stage, dout, s);
+  if (e == hipSuccess && out_location == H2S_LOC_HOST) e = hipMemcpyAsync(out_rgb, dout, ob, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (din_mem) hipFree(din_mem);
+  if (out_location == H2S_LOC_HOST) hipFree(dout);
+  if (e != hipSuccess) return hip_fail(c, e, "debug kernel");
+  return 0;
+}
+
+int h2s_set_timing(h2s_ctx* c, int enabled) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  c->timing = enabled != 0;
+  c->ev_count = 0;
+  return 0;
+}
+
+double h2s_kernel_ms(h2s_ctx* c, int count) {
+  if (!c) return -1.0;
+  if (count <= 0) {
+    c->ev_count = 0;
+    return 0.0;
+  }
+  DeviceGuard g(c->device);
+  const long long avail = c->ev_count < kEvRing ? c->ev_count : kEvRing;
+  if (count > avail) count = (int)avail;
+  if (count == 0) return 0.0;
+  double sum = 0.0;
+  for (int i = 0; i < count; i++) {
+    const int slot = (int)((c->ev_count - 1 - i) % kEvRing);
+    if (hipEventSynchronize(c->ev1[slot]) != hipSuccess) return -1.0;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, c->ev0[slot], c->ev1[slot]) != hipSuccess) return -1.0;
+    sum += ms;
+  }
+  return sum / count;
+}
+
+}  // extern "C"

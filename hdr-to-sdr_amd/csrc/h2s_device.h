@@ -1,0 +1,237 @@
+// h2s_device.h — per-pixel chain for gfx950 (device code) and the launch
+// parameter block shared by the kernels and the host launcher.
+//
+// Stage numbering follows the reference chain string (src/utils.py:38-42):
+//   S1 zscale=t=linear:npl=100   S2 tonemap={tm}   S3 zscale=t=bt709
+//   S4 lut3d=interp=tetrahedral  S6 (auto) scale->yuv420p  S7 eq=gamma
+//   S8 (auto) scale->-pix_fmt (src/ffmpeg_command.py:355-360)
+// The CPU statement each function must agree with is oracle/h2s_oracle.c.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace h2s {
+
+struct KParams {
+  // geometry (luma W x H, chroma cw x ch, ngx groups of QPT chroma columns)
+  int W, H, cw, ch, ngx;
+  int nframes;
+  long long total;  // nframes * ch * ngx work items
+  const uint8_t* in[3];
+  long long in_ls[3], in_fp[3];
+  uint8_t* out[3];
+  long long out_ls[3], out_fp[3];
+  // S1: zimg depth conversion, BT.2020-NCL matrix, transfer
+  float y_scale, y_off, c_scale, c_off;
+  float m_rcr, m_gcb, m_gcr, m_bcb;
+  float lin_scale;
+  int transfer;  // h2s_transfer
+  // S2: vf_tonemap
+  int tonemap;  // h2s_tonemap
+  int desat_on;
+  float desat, lr, lg, lb;
+  float lin_k;          // LINEAR: param/peak
+  float gam_inv_peak, gam_inv_param, gam_low_k;  // GAMMA
+  float clip_k;         // CLIP: param
+  float hable_peak_inv; // HABLE: 1/hable(peak)
+  float rein_p, rein_k; // REINHARD: param, (peak+param)/peak
+  float mob_j, mob_a, mob_b, mob_k;  // MOBIUS
+  float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum;  // BT2390
+  float npl_1e4, e4_npl;  // npl/10000, 10000/npl
+  // S3/S4
+  int lut_enabled, lut_n, lut_sg, lut_sb;
+  float lut_max;
+  const float4* lut;
+  float m709[9];
+  // S6..S8
+  int qmax, shift_out;
+  float qscale;
+  int eq_identity;
+  const uint16_t* eq_lut;
+  // Y'CbCr 709 rows
+  float k709[3], kcb[3], kcr[3];
+};
+
+// ---- fast transcendentals (v_log_f32 / v_exp_f32 / v_rcp_f32) ----------
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// x^p for x >= 0 (x == 0 -> 0 for p > 0)
+__device__ __forceinline__ float fpow(float x, float p) { return fexp2(p * flog2(x)); }
+__device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
+
+// ST 2084 constants (exact binary values, as zimg defines them)
+#define PQ_M1 0.1593017578125f
+#define PQ_M2 78.84375f
+#define PQ_C1 0.8359375f
+#define PQ_C2 18.8515625f
+#define PQ_C3 18.6875f
+#define HLG_A 0.17883277f
+#define HLG_B 0.28466892f
+#define HLG_C 0.55991073f
+
+// S1 transfer: zimg st_2084_eotf (normalised, 1.0 = 10000 nits)
+__device__ __forceinline__ float pq_eotf(float x) {
+  if (!(x > 0.0f)) return 0.0f;
+  float xpow = fpow(x, 1.0f / PQ_M2);
+  float num = fmaxf(xpow - PQ_C1, 0.0f);
+  float den = fmaxf(PQ_C2 - PQ_C3 * xpow, 1.17549435e-38f);
+  return fpow(num * frcp(den), 1.0f / PQ_M1);
+}
+
+// ST 2084 inverse EOTF (BT.2390 works in the PQ domain)
+__device__ __forceinline__ float pq_encode(float y) {
+  float ym = fpow(fmaxf(y, 0.0f), PQ_M1);
+  return fpow((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym), PQ_M2);
+}
+
+// zimg arib_b67_inverse_oetf
+__device__ __forceinline__ float hlg_inv_oetf(float x) {
+  x = fmaxf(x, 0.0f);
+  if (x <= 0.5f) return (x * x) * (1.0f / 3.0f);
+  return (fexp2((x - HLG_C) * (1.0f / HLG_A) * 1.44269504f) + HLG_B) * (1.0f / 12.0f);
+}
+
+// vf_tonemap hable()
+__device__ __forceinline__ float hable(float in) {
+  const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
+  return (in * (in * a + b * c) + d * e) * frcp(in * (in * a + b) + d * f) - e / f;
+}
+
+// S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)
+__device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g, float& b) {
+  float sig, sig_orig;
+  if (P.tonemap == 7 /* BT2390 */) {
+    sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
+    float e1n = (pq_encode(sig * P.npl_1e4) - P.b_srcmin) * P.b_inv_range;
+    float e2 = e1n;
+    if (P.b_ks < 1.0f && e1n > P.b_ks) {
+      float t = (e1n - P.b_ks) * P.b_inv_1mks;
+      float t2 = t * t, t3 = t2 * t;
+      e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * P.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - P.b_ks) +
+           (-2.0f * t3 + 3.0f * t2) * P.b_maxlum;
+    }
+    float s2 = pq_eotf(e2 * P.b_range + P.b_srcmin) * P.e4_npl;
+    float k = s2 * frcp(sig);
+    r *= k, g *= k, b *= k;
+    return;
+  }
+  if (P.desat_on) {
+    float luma = P.lr * r + P.lg * g + P.lb * b;
+    float ob = fmaxf(luma - P.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
+    r = r * (1.0f - ob) + luma * ob;
+    g = g * (1.0f - ob) + luma * ob;
+    b = b * (1.0f - ob) + luma * ob;
+  }
+  sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
+  sig_orig = sig;
+  switch (P.tonemap) {
+    case 1:  // LINEAR
+      sig = sig * P.lin_k;
+      break;
+    case 2:  // GAMMA
+      sig = sig > 0.05f ? fpow(sig * P.gam_inv_peak, P.gam_inv_param) : sig * P.gam_low_k;
+      break;
+    case 3:  // CLIP
+      sig = clamp01(sig * P.clip_k);
+      break;
+    case 4:  // REINHARD
+      sig = sig * frcp(sig + P.rein_p) * P.rein_k;
+      break;
+    case 5:  // HABLE
+      sig = hable(sig) * P.hable_peak_inv;
+      break;
+    case 6:  // MOBIUS
+      sig = sig <= P.mob_j ? sig : P.mob_k * (sig + P.mob_a) * frcp(sig + P.mob_b);
+      break;
+    default:
+      break;
+  }
+  float k = sig * frcp(sig_orig);
+  r *= k, g *= k, b *= k;
+}
+
+// S3: zimg rec_1886_inverse_eotf
+__device__ __forceinline__ float bt1886_inv(float x) {
+  return x > 0.0f ? fpow(x, 1.0f / 2.4f) : 0.0f;
+}
+
+// S4: vf_lut3d sanitizef + clip + interp_tetrahedral.  The lattice is in
+// .cube order (red fastest): index(r,g,b) = r + g*N + b*N^2.  Case selection
+// uses the same strict comparisons as interp_tetrahedral, expressed as
+// selects instead of branches (no divergence); the weights and the term order
+// are the reference's.
+__device__ __forceinline__ float lut_coord(float x, float lut_max) {
+  x = (x == x) ? x : 0.0f;  // NaN -> 0 (sanitizef); +-inf clip below
+  return __builtin_amdgcn_fmed3f(x * lut_max, 0.0f, lut_max);
+}
+
+__device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g, float& b) {
+  const float sr = lut_coord(r, P.lut_max), sg = lut_coord(g, P.lut_max), sb = lut_coord(b, P.lut_max);
+  const int pr = (int)sr, pg = (int)sg, pb = (int)sb;
+  const int last = P.lut_n - 1;
+  const int str = pr < last ? 1 : 0;
+  const int stg = pg < last ? P.lut_sg : 0;
+  const int stb = pb < last ? P.lut_sb : 0;
+  const float dr = sr - (float)pr, dg = sg - (float)pg, db = sb - (float)pb;
+  const bool rg = dr > dg, gb = dg > db, rb = dr > db, bg = db > dg, br = db > dr;
+  float x1, x2, x3;
+  int o1, o2;
+  if (rg) {
+    if (gb) { x1 = dr; x2 = dg; x3 = db; o1 = str; o2 = stg; }
+    else if (rb) { x1 = dr; x2 = db; x3 = dg; o1 = str; o2 = stb; }
+    else { x1 = db; x2 = dr; x3 = dg; o1 = stb; o2 = str; }
+  } else {
+    if (bg) { x1 = db; x2 = dg; x3 = dr; o1 = stb; o2 = stg; }
+    else if (br) { x1 = dg; x2 = db; x3 = dr; o1 = stg; o2 = stb; }
+    else { x1 = dg; x2 = dr; x3 = db; o1 = stg; o2 = str; }
+  }
+  const int base = pr + pg * P.lut_sg + pb * P.lut_sb;
+  const float4 c000 = P.lut[base];
+  const float4 c1 = P.lut[base + o1];
+  const float4 c2 = P.lut[base + o1 + o2];
+  const float4 c111 = P.lut[base + str + stg + stb];
+  const float w0 = 1.0f - x1, w1 = x1 - x2, w2 = x2 - x3, w3 = x3;
+  r = w0 * c000.x + w1 * c1.x + w2 * c2.x + w3 * c111.x;
+  g = w0 * c000.y + w1 * c1.y + w2 * c2.y + w3 * c111.y;
+  b = w0 * c000.z + w1 * c1.z + w2 * c2.z + w3 * c111.z;
+}
+
+// S1 (after upsampling) .. S4 on one pixel.  UPTO = last stage to apply.
+template <int UPTO>
+__device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, float cr, float& r, float& g,
+                                         float& b) {
+  float er = y + P.m_rcr * cr;
+  float eg = y + P.m_gcb * cb + P.m_gcr * cr;
+  float eb = y + P.m_bcb * cb;
+  if (P.transfer == 1) {  // HLG: inverse OETF + OOTF (gamma 1.2 at 1000 nits)
+    r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), b = hlg_inv_oetf(eb);
+    float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
+    float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
+    r *= w, g *= w, b *= w;
+  } else {
+    r = pq_eotf(er) * P.lin_scale;
+    g = pq_eotf(eg) * P.lin_scale;
+    b = pq_eotf(eb) * P.lin_scale;
+  }
+  if (UPTO == 1) return;
+  tonemap_px(P, r, g, b);
+  if (UPTO == 2) return;
+  if (P.lut_enabled) {
+    r = bt1886_inv(r), g = bt1886_inv(g), b = bt1886_inv(b);
+    if (UPTO == 3) return;
+    lut3d_tetra(P, r, g, b);
+  } else {
+    float mr = P.m709[0] * r + P.m709[1] * g + P.m709[2] * b;
+    float mg = P.m709[3] * r + P.m709[4] * g + P.m709[5] * b;
+    float mb = P.m709[6] * r + P.m709[7] * g + P.m709[8] * b;
+    r = clamp01(bt1886_inv(mr)), g = clamp01(bt1886_inv(mg)), b = clamp01(bt1886_inv(mb));
+  }
+}
+
+__device__ __forceinline__ int quant(float v, int qmax) {
+  int i = (int)floorf(v + 0.5f);
+  return min(max(i, 0), qmax);
+}
+
+}  // namespace h2s

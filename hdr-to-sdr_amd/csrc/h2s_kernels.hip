@@ -1,0 +1,256 @@
+// h2s_kernels.hip — gfx950 kernels for the HDR->SDR hot path.
+//
+// k_process: the whole per-frame chain of src/utils.py:38-42 fused into one
+// pass over HBM: read packed 10/12-bit planar 4:2:0, upsample chroma, S1..S4
+// per pixel, RGB->Y'CbCr, 2x2 chroma reduction, quantise, eq, write 4:2:0.
+// One work item = QPT horizontally adjacent 2x2 luma quads (one output chroma
+// sample each) of one chroma row of one frame; the flattened item index runs
+// columns fastest, so a wavefront reads contiguous row segments (16-B Y loads,
+// 8-B chroma loads per lane).  Blocks are remapped so that each XCD walks a
+// contiguous range of rows (chroma halo rows and LUT lines stay in its L2).
+#include <hip/hip_runtime.h>
+
+#include "h2s_device.h"
+
+namespace h2s {
+
+__device__ __forceinline__ int edge(int i, int n) {
+  // zimg bilinear edge rule (see oracle/h2s_oracle.c edge())
+  i = i < 0 ? -i : i;
+  return i > n - 1 ? n - 1 : i;
+}
+
+// XCD-aware block remap: hardware deals blocks round-robin over 8 XCDs;
+// give XCD x the contiguous logical range [x*per(+rem), ...).  Bijective.
+__device__ __forceinline__ long long xcd_remap(long long b, long long nb) {
+  const long long xcd = b & 7, idx = b >> 3, per = nb >> 3, rem = nb & 7;
+  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
+__device__ __forceinline__ int ld16(const uint8_t* row, int x) {
+  return *reinterpret_cast<const uint16_t*>(row + 2 * x);
+}
+
+template <int QPT, bool VEC, bool OUT8>
+__global__ __launch_bounds__(256) void k_process(const KParams P) {
+  const long long lb = xcd_remap(blockIdx.x, gridDim.x);
+  const long long item = lb * 256 + threadIdx.x;
+  if (item >= P.total) return;
+  const int gx = (int)(item % P.ngx);
+  const long long t = item / P.ngx;
+  const int cy = (int)(t % P.ch);
+  const int f = (int)(t / P.ch);
+  const int cx0 = gx * QPT;
+  const int cw = P.cw, ch = P.ch;
+
+  // ---- chroma: rows cy-1, cy, cy+1; columns cx0 .. cx0+QPT (halo) ----
+  float cu[3][QPT + 1], cv[3][QPT + 1];
+  const int crow[3] = {edge(cy - 1, ch), cy, edge(cy + 1, ch)};
+  const bool full = cx0 + QPT <= cw;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const uint8_t* ru = P.in[1] + f * P.in_fp[1] + crow[i] * P.in_ls[1];
+    const uint8_t* rv = P.in[2] + f * P.in_fp[2] + crow[i] * P.in_ls[2];
+    if (VEC && full && QPT == 4) {
+      const uint2 a = *reinterpret_cast<const uint2*>(ru + 2 * cx0);
+      const uint2 b = *reinterpret_cast<const uint2*>(rv + 2 * cx0);
+      const int hx = cx0 + 4 < cw ? cx0 + 4 : cw - 1;
+      int su[5] = {(int)(a.x & 0xffff), (int)(a.x >> 16), (int)(a.y & 0xffff), (int)(a.y >> 16), ld16(ru, hx)};
+      int sv[5] = {(int)(b.x & 0xffff), (int)(b.x >> 16), (int)(b.y & 0xffff), (int)(b.y >> 16), ld16(rv, hx)};
+#pragma unroll
+      for (int k = 0; k <= QPT; k++) {
+        cu[i][k] = (float)su[k] * P.c_scale + P.c_off;
+        cv[i][k] = (float)sv[k] * P.c_scale + P.c_off;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k <= QPT; k++) {
+        const int x = cx0 + k < cw ? cx0 + k : cw - 1;
+        cu[i][k] = (float)ld16(ru, x) * P.c_scale + P.c_off;
+        cv[i][k] = (float)ld16(rv, x) * P.c_scale + P.c_off;
+      }
+    }
+  }
+  // horizontal pass (left siting): h[2k] = c[k], h[2k+1] = (c[k] + c[k+1]) / 2
+  float hu[3][2 * QPT], hv[3][2 * QPT];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int k = 0; k < QPT; k++) {
+      hu[i][2 * k] = cu[i][k];
+      hu[i][2 * k + 1] = 0.5f * cu[i][k] + 0.5f * cu[i][k + 1];
+      hv[i][2 * k] = cv[i][k];
+      hv[i][2 * k + 1] = 0.5f * cv[i][k] + 0.5f * cv[i][k + 1];
+    }
+
+  // ---- luma: rows 2cy, 2cy+1; columns 2cx0 .. 2cx0+2QPT-1 ----
+  const int x0 = 2 * cx0;
+  int ys[2][2 * QPT];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint8_t* ry = P.in[0] + f * P.in_fp[0] + (2 * cy + j) * P.in_ls[0];
+    if (VEC && full && QPT == 4) {
+      const uint4 a = *reinterpret_cast<const uint4*>(ry + 2 * x0);
+      const unsigned w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        ys[j][2 * k] = (int)(w[k] & 0xffff);
+        ys[j][2 * k + 1] = (int)(w[k] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 * QPT; k++) {
+        const int x = x0 + k < P.W ? x0 + k : P.W - 1;
+        ys[j][k] = ld16(ry, x);
+      }
+    }
+  }
+
+  // ---- per pixel chain, Y'CbCr, quantise ----
+  int yo[2][2 * QPT], uo[QPT], vo[QPT];
+#pragma unroll
+  for (int k = 0; k < QPT; k++) {
+    float cbs[4], crs[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int j = p >> 1, x = 2 * k + (p & 1);
+      const float cb = j == 0 ? 0.25f * hu[0][x] + 0.75f * hu[1][x] : 0.75f * hu[1][x] + 0.25f * hu[2][x];
+      const float cr = j == 0 ? 0.25f * hv[0][x] + 0.75f * hv[1][x] : 0.75f * hv[1][x] + 0.25f * hv[2][x];
+      const float yv = (float)ys[j][x] * P.y_scale + P.y_off;
+      float r, g, b;
+      chain_px<4>(P, yv, cb, cr, r, g, b);
+      r = clamp01(r), g = clamp01(g), b = clamp01(b);
+      const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
+      cbs[p] = P.kcb[0] * r + P.kcb[1] * g + P.kcb[2] * b;
+      crs[p] = P.kcr[0] * r + P.kcr[1] * g + P.kcr[2] * b;
+      int yq = quant((16.0f + 219.0f * Y) * P.qscale, P.qmax);
+      if (!P.eq_identity) yq = P.eq_lut[yq];
+      yo[j][x] = yq << P.shift_out;
+    }
+    const float cb = ((cbs[0] + cbs[1]) + (cbs[2] + cbs[3])) * 0.25f;
+    const float cr = ((crs[0] + crs[1]) + (crs[2] + crs[3])) * 0.25f;
+    uo[k] = quant((128.0f + 224.0f * cb) * P.qscale, P.qmax) << P.shift_out;
+    vo[k] = quant((128.0f + 224.0f * cr) * P.qscale, P.qmax) << P.shift_out;
+  }
+
+  // ---- stores ----
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    uint8_t* ry = P.out[0] + f * P.out_fp[0] + (2 * cy + j) * P.out_ls[0];
+    if (VEC && full && QPT == 4) {
+      if (OUT8) {
+        uint2 w;
+        w.x = (unsigned)yo[j][0] | ((unsigned)yo[j][1] << 8) | ((unsigned)yo[j][2] << 16) | ((unsigned)yo[j][3] << 24);
+        w.y = (unsigned)yo[j][4] | ((unsigned)yo[j][5] << 8) | ((unsigned)yo[j][6] << 16) | ((unsigned)yo[j][7] << 24);
+        *reinterpret_cast<uint2*>(ry + x0) = w;
+      } else {
+        uint4 w;
+        w.x = (unsigned)yo[j][0] | ((unsigned)yo[j][1] << 16);
+        w.y = (unsigned)yo[j][2] | ((unsigned)yo[j][3] << 16);
+        w.z = (unsigned)yo[j][4] | ((unsigned)yo[j][5] << 16);
+        w.w = (unsigned)yo[j][6] | ((unsigned)yo[j][7] << 16);
+        *reinterpret_cast<uint4*>(ry + 2 * x0) = w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 * QPT; k++) {
+        if (x0 + k < P.W) {
+          if (OUT8) ry[x0 + k] = (uint8_t)yo[j][k];
+          else reinterpret_cast<uint16_t*>(ry)[x0 + k] = (uint16_t)yo[j][k];
+        }
+      }
+    }
+  }
+  uint8_t* ru = P.out[1] + f * P.out_fp[1] + cy * P.out_ls[1];
+  uint8_t* rv = P.out[2] + f * P.out_fp[2] + cy * P.out_ls[2];
+  if (VEC && full && QPT == 4) {
+    if (OUT8) {
+      *reinterpret_cast<unsigned*>(ru + cx0) =
+          (unsigned)uo[0] | ((unsigned)uo[1] << 8) | ((unsigned)uo[2] << 16) | ((unsigned)uo[3] << 24);
+      *reinterpret_cast<unsigned*>(rv + cx0) =
+          (unsigned)vo[0] | ((unsigned)vo[1] << 8) | ((unsigned)vo[2] << 16) | ((unsigned)vo[3] << 24);
+    } else {
+      uint2 a, b;
+      a.x = (unsigned)uo[0] | ((unsigned)uo[1] << 16);
+      a.y = (unsigned)uo[2] | ((unsigned)uo[3] << 16);
+      b.x = (unsigned)vo[0] | ((unsigned)vo[1] << 16);
+      b.y = (unsigned)vo[2] | ((unsigned)vo[3] << 16);
+      *reinterpret_cast<uint2*>(ru + 2 * cx0) = a;
+      *reinterpret_cast<uint2*>(rv + 2 * cx0) = b;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < QPT; k++) {
+      if (cx0 + k < cw) {
+        if (OUT8) {
+          ru[cx0 + k] = (uint8_t)uo[k];
+          rv[cx0 + k] = (uint8_t)vo[k];
+        } else {
+          reinterpret_cast<uint16_t*>(ru)[cx0 + k] = (uint16_t)uo[k];
+          reinterpret_cast<uint16_t*>(rv)[cx0 + k] = (uint16_t)vo[k];
+        }
+      }
+    }
+  }
+}
+
+// Debug/parity kernel: float RGB of frame 0 after stage STAGE, one thread per
+// pixel, generic (unvectorised) sample access.
+template <int STAGE>
+__global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long npx = (long long)P.W * P.H;
+  if (i >= npx) return;
+  const int x = (int)(i % P.W), y = (int)(i / P.W);
+  const int cw = P.cw, ch = P.ch;
+  auto hpass = [&](int plane, int cyy) -> float {
+    const uint8_t* row = P.in[plane] + edge(cyy, ch) * P.in_ls[plane];
+    const int k = x >> 1;
+    const float a = (float)ld16(row, edge(k, cw)) * P.c_scale + P.c_off;
+    if (!(x & 1)) return a;
+    const float b = (float)ld16(row, edge(k + 1, cw)) * P.c_scale + P.c_off;
+    return 0.5f * a + 0.5f * b;
+  };
+  auto up = [&](int plane) -> float {
+    const int m = y >> 1;
+    if (!(y & 1)) return 0.25f * hpass(plane, m - 1) + 0.75f * hpass(plane, m);
+    return 0.75f * hpass(plane, m) + 0.25f * hpass(plane, m + 1);
+  };
+  const float cb = up(1), cr = up(2);
+  const float yv = (float)ld16(P.in[0] + y * P.in_ls[0], x) * P.y_scale + P.y_off;
+  float r, g, b;
+  chain_px<STAGE>(P, yv, cb, cr, r, g, b);
+  out[i] = r;
+  out[npx + i] = g;
+  out[2 * npx + i] = b;
+}
+
+// ---- host-side launchers (called from h2s_api.hip) ----------------------
+hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s) {
+  constexpr int QPT = 4;
+  const long long nb = (P.total + 255) / 256;
+  if (nb == 0) return hipSuccess;
+  dim3 grid((unsigned)nb), block(256);
+  if (vec) {
+    if (out8) hipLaunchKernelGGL((k_process<QPT, true, true>), grid, block, 0, s, P);
+    else hipLaunchKernelGGL((k_process<QPT, true, false>), grid, block, 0, s, P);
+  } else {
+    if (out8) hipLaunchKernelGGL((k_process<QPT, false, true>), grid, block, 0, s, P);
+    else hipLaunchKernelGGL((k_process<QPT, false, false>), grid, block, 0, s, P);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s) {
+  const long long npx = (long long)P.W * P.H;
+  dim3 grid((unsigned)((npx + 255) / 256)), block(256);
+  switch (stage) {
+    case 1: hipLaunchKernelGGL((k_debug<1>), grid, block, 0, s, P, out); break;
+    case 2: hipLaunchKernelGGL((k_debug<2>), grid, block, 0, s, P, out); break;
+    case 3: hipLaunchKernelGGL((k_debug<3>), grid, block, 0, s, P, out); break;
+    default: hipLaunchKernelGGL((k_debug<4>), grid, block, 0, s, P, out); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace h2s

@@ -1,0 +1,153 @@
+"""ctypes binding of libh2s (include/h2s.h).
+
+The library is the product: every pixel this package produces comes from its
+HIP kernels.  There is no Python or CPU fallback for the pixel path — if the
+shared object is missing or a GPU call fails, the error propagates.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libh2s.so')
+
+# ---- error codes (include/h2s.h) ------------------------------------------
+H2S_OK = 0
+H2S_E_INVALID_ARG = -1
+H2S_E_UNSUPPORTED = -2
+H2S_E_HIP = -3
+H2S_E_OOM = -4
+H2S_E_LUT_MISSING = -5
+H2S_E_PARSE = -6
+
+TRC_PQ, TRC_HLG = 0, 1
+TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS, TM_BT2390 = range(8)
+MODE_COMPAT8, MODE_NATIVE = 0, 1
+DESAT_LUMA_RGB, DESAT_LUMA_BT2020, DESAT_LUMA_BT709 = 0, 1, 2
+LOC_DEVICE, LOC_HOST = 0, 1
+STAGE_LINEAR, STAGE_TONEMAP, STAGE_GAMMA, STAGE_LUT = 1, 2, 3, 4
+
+# every symbol include/h2s.h declares (checked by tests/test_abi_exports.py)
+EXPORTS = (
+    'h2s_abi_version', 'h2s_create', 'h2s_destroy', 'h2s_last_error',
+    'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
+    'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
+    'h2s_kernel_ms', 'h2s_set_timing',
+)
+
+
+class H2SParams(ctypes.Structure):
+    _fields_ = [
+        ('transfer_in', ctypes.c_int32),
+        ('bits_in', ctypes.c_int32),
+        ('bits_out', ctypes.c_int32),
+        ('tonemap', ctypes.c_int32),
+        ('tm_param', ctypes.c_double),
+        ('desat', ctypes.c_double),
+        ('peak', ctypes.c_double),
+        ('npl', ctypes.c_double),
+        ('gamma', ctypes.c_double),
+        ('maxcll', ctypes.c_double),
+        ('mastering_max', ctypes.c_double),
+        ('lut_enabled', ctypes.c_int32),
+        ('mode', ctypes.c_int32),
+        ('desat_luma', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 5),
+    ]
+
+
+class H2SFrames(ctypes.Structure):
+    _fields_ = [
+        ('data', ctypes.c_void_p * 3),
+        ('linesize', ctypes.c_int64 * 3),
+        ('frame_pitch', ctypes.c_int64 * 3),
+        ('width', ctypes.c_int32),
+        ('height', ctypes.c_int32),
+        ('bits', ctypes.c_int32),
+        ('location', ctypes.c_int32),
+    ]
+
+
+class H2SError(RuntimeError):
+    """A libh2s call failed (HIP error, OOM, ...).  Subclasses RuntimeError:
+    the reference surfaces a failed ffmpeg run as RuntimeError
+    (src/utils.py:297-308)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f'libh2s error {code}: {msg}')
+        self.code = code
+
+
+def raise_for(code: int, msg: str) -> None:
+    """Map an H2S_E_* code onto the reference's exception types."""
+    if code == H2S_OK:
+        return
+    if code == H2S_E_LUT_MISSING:
+        # src/utils.py:185-186: a missing bundled LUT is FileNotFoundError
+        raise FileNotFoundError(msg)
+    if code in (H2S_E_INVALID_ARG, H2S_E_UNSUPPORTED, H2S_E_PARSE):
+        # src/ffmpeg_command.py:240-245: an impossible request is ValueError
+        raise ValueError(msg)
+    raise H2SError(code, msg)
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libh2s once.  Raises ImportError when the extension was not
+    built — the pixel path has no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f'libh2s.so not found at {LIB_PATH}; build it with '
+            '`python -c "import __graft_entry__ as g; g.build()"` (hipcc, gfx950)')
+    # torch ships its own libamdhip64 with the same SONAME; importing torch
+    # first makes libh2s bind to that single HIP runtime instead of loading a
+    # second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    c_ctx = ctypes.c_void_p
+    sig = {
+        'h2s_abi_version': (ctypes.c_int, []),
+        'h2s_create': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_ctx)]),
+        'h2s_destroy': (None, [c_ctx]),
+        'h2s_last_error': (ctypes.c_char_p, [c_ctx]),
+        'h2s_set_lut': (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int]),
+        'h2s_params_default': (None, [ctypes.POINTER(H2SParams)]),
+        'h2s_set_params': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SParams)]),
+        'h2s_process': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.POINTER(H2SFrames),
+                                       ctypes.c_int, ctypes.c_void_p]),
+        'h2s_debug_float': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+        'h2s_cube_generate': (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+        'h2s_cube_format': (ctypes.c_int64, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int64]),
+        'h2s_cube_parse': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]),
+        'h2s_kernel_ms': (ctypes.c_double, [c_ctx, ctypes.c_int]),
+        'h2s_set_timing': (ctypes.c_int, [c_ctx, ctypes.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.h2s_abi_version() != 1:
+        raise ImportError(f'libh2s ABI {L.h2s_abi_version()} != 1')
+    _lib = L
+    return L
+
+
+def default_params() -> H2SParams:
+    p = H2SParams()
+    lib().h2s_params_default(ctypes.byref(p))
+    return p
+
+
+NAN = math.nan

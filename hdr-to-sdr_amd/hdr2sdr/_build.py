@@ -1,0 +1,73 @@
+"""In-tree build of libh2s.so (hipcc, gfx950) and of the test oracle.
+
+The .so files land next to their loaders (hdr2sdr/libh2s.so,
+oracle/build/liboracle.so): git-ignored, but they travel to the GPU box with
+the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+PROJ_DIR = os.path.dirname(PKG_DIR)            # hdr-to-sdr_amd/
+REPO_DIR = os.path.dirname(PROJ_DIR)
+CSRC = os.path.join(PROJ_DIR, 'csrc')
+INCLUDE = os.path.join(REPO_DIR, 'include')
+LIB = os.path.join(PKG_DIR, 'libh2s.so')
+ORACLE_DIR = os.path.join(REPO_DIR, 'oracle')
+ORACLE_LIB = os.path.join(ORACLE_DIR, 'build', 'liboracle.so')
+
+ARCH = os.environ.get('H2S_OFFLOAD_ARCH', 'gfx950')
+SOURCES = ['h2s_api.hip', 'h2s_kernels.hip', 'h2s_cube.cpp']
+HEADERS = ['h2s_device.h']
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError('hipcc not found (ROCm toolchain required to build libh2s)')
+
+
+def _stale(target: str, deps: 'list[str]') -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, 'h2s.h')]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    tmp = LIB + f'.tmp{os.getpid()}'
+    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC',
+           '-Wno-unused-value', '-Wno-unused-result', '-o', tmp] + srcs
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False, verbose: bool = False) -> str:
+    src = os.path.join(ORACLE_DIR, 'h2s_oracle.c')
+    deps = [src, os.path.join(INCLUDE, 'h2s.h')]
+    if not force and not _stale(ORACLE_LIB, deps):
+        return ORACLE_LIB
+    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
+    tmp = ORACLE_LIB + f'.tmp{os.getpid()}'
+    cmd = ['gcc', '-O2', '-std=c11', '-fopenmp', '-shared', '-fPIC', '-o', tmp, src, '-lm']
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_lib(force, verbose)
+    build_oracle(force, verbose)

@@ -1,0 +1,235 @@
+"""The reference's filter-chain interface, mirrored.
+
+The reference selects its hot path as a string: ``FFMPEG_CONVERT_FILTER``
+(src/utils.py:38-42) formatted with ``gamma``, ``tonemapper`` and the LUT path
+by ``ffmpeg_command._filter_args`` (src/ffmpeg_command.py:227-247), from the
+fields of ``ConversionRequest`` (src/conversion.py:26-44).  This module keeps
+those names and semantics and turns either a request or a chain string into
+the ``TonemapParams`` the HIP engine executes:
+
+* ``TONEMAP`` / ``GPU_ONLY_TONEMAPPERS`` / ``is_gpu_only_tonemapper`` —
+  src/utils.py:16, :67-73.
+* ``FFMPEG_CONVERT_FILTER`` — src/utils.py:38-42 (the same template, so a
+  chain built by the reference parses here unchanged).
+* ``TonemapParams.from_request`` — what ``_filter_args`` + ``_codec_and_pix_fmt``
+  decide for one request (tonemapper lower-cased :235, pix_fmt :355-360).
+* ``parse_filter_chain`` — the drop-in: any chain string the reference
+  builds (CPU chain, legacy no-LUT preview chain) maps onto one kernel launch.
+"""
+from __future__ import annotations
+
+import math
+import re
+from dataclasses import dataclass, replace
+from typing import Any
+
+from . import _abi
+
+# src/utils.py:16
+TONEMAP = ["Reinhard", "Mobius", "Hable", "BT.2390", "Spline"]
+
+# src/utils.py:38-42 (template kept verbatim: it is the interface)
+FFMPEG_CONVERT_FILTER = (
+    'zscale=t=linear:npl=100,tonemap={tonemapper},zscale=t=bt709:m=bt709:r=tv,'
+    'lut3d=file={lut_path}:interp=tetrahedral,setparams=color_primaries=bt709:color_trc=bt709:colorspace=bt709,'
+    'eq=gamma={gamma}'
+)
+
+# src/utils.py:67.  The reference can only run these through libplacebo; this
+# engine runs BT.2390 natively on the GPU, Spline is not implemented.
+GPU_ONLY_TONEMAPPERS = {'bt.2390', 'spline'}
+
+_TM_NAMES = {
+    'none': _abi.TM_NONE, 'linear': _abi.TM_LINEAR, 'gamma': _abi.TM_GAMMA,
+    'clip': _abi.TM_CLIP, 'reinhard': _abi.TM_REINHARD, 'hable': _abi.TM_HABLE,
+    'mobius': _abi.TM_MOBIUS, 'bt.2390': _abi.TM_BT2390, 'bt2390': _abi.TM_BT2390,
+}
+_TRC_NAMES = {'smpte2084': _abi.TRC_PQ, 'pq': _abi.TRC_PQ,
+              'arib-std-b67': _abi.TRC_HLG, 'hlg': _abi.TRC_HLG}
+_MODES = {'compat8': _abi.MODE_COMPAT8, 'native': _abi.MODE_NATIVE}
+_DESAT_LUMA = {'rgb': _abi.DESAT_LUMA_RGB, 'bt2020': _abi.DESAT_LUMA_BT2020,
+               'bt709': _abi.DESAT_LUMA_BT709}
+
+
+def is_gpu_only_tonemapper(tonemapper: str) -> bool:
+    """src/utils.py:70-73: case-insensitive membership test."""
+    return tonemapper.lower() in GPU_ONLY_TONEMAPPERS
+
+
+@dataclass(frozen=True)
+class TonemapParams:
+    """Everything one kernel launch needs besides the LUT lattice.
+
+    Defaults are the reference chain's: npl=100, vf_tonemap's desat 2.0 and
+    automatic peak, tetrahedral LUT on, eq gamma 1.0, and the settings
+    defaults (src/settings.py:10-26: Mobius)."""
+    tonemapper: str = 'mobius'
+    gamma: float = 1.0
+    bits_in: int = 10
+    bits_out: int = 10
+    transfer: str = 'smpte2084'
+    lut_enabled: bool = True
+    mode: str = 'compat8'
+    tm_param: float = math.nan
+    desat: float = 2.0
+    peak: float = 0.0
+    npl: float = 100.0
+    maxcll: float = 0.0
+    mastering_max: float = 0.0
+    desat_luma: str = 'rgb'
+
+    def __post_init__(self) -> None:
+        tm = self.tonemapper.lower()
+        if tm == 'spline':
+            raise ValueError("spline tone mapping is libplacebo-only and not implemented by this engine; "
+                             "choose reinhard, mobius, hable or bt.2390")
+        if tm not in _TM_NAMES:
+            raise ValueError(f'unknown tonemapper {self.tonemapper!r}')
+        if self.transfer not in _TRC_NAMES:
+            raise ValueError(f'unknown input transfer {self.transfer!r}')
+        if self.mode not in _MODES:
+            raise ValueError(f'unknown mode {self.mode!r}')
+        if self.desat_luma not in _DESAT_LUMA:
+            raise ValueError(f'unknown desat_luma {self.desat_luma!r}')
+        if self.bits_in not in (10, 12):
+            raise ValueError(f'bits_in must be 10 or 12, got {self.bits_in}')
+        if self.bits_out not in (8, 10, 12):
+            raise ValueError(f'bits_out must be 8, 10 or 12, got {self.bits_out}')
+        if not self.gamma > 0:
+            raise ValueError(f'gamma must be > 0, got {self.gamma}')
+
+    # ---- construction from the reference's request ---------------------
+    @classmethod
+    def from_request(cls, request: Any, bits_in: int = 10, transfer: str = 'smpte2084',
+                     **overrides: Any) -> 'TonemapParams':
+        """Map a ConversionRequest-like object (src/conversion.py:26-44).
+
+        * tonemapper: lower-cased as _filter_args does (src/ffmpeg_command.py:235).
+        * bit_depth -> output depth (src/ffmpeg_command.py:355-360; 8 -> yuv420p).
+        * lut_enabled: the CPU chain always applies the LUT
+          (src/utils.py:61-66 comment; construct_ffmpeg_command ignores it),
+          so it is honoured only when explicitly overridden.
+        """
+        bit_depth = int(getattr(request, 'bit_depth', 8))
+        bits_out = 12 if bit_depth >= 12 else (10 if bit_depth == 10 else 8)
+        kw = dict(tonemapper=str(request.tonemapper).lower(), gamma=float(request.gamma),
+                  bits_in=bits_in, bits_out=bits_out, transfer=transfer, lut_enabled=True)
+        kw.update(overrides)
+        return cls(**kw)
+
+    def with_(self, **kw: Any) -> 'TonemapParams':
+        return replace(self, **kw)
+
+    # ---- C struct ---------------------------------------------------------
+    def to_c(self) -> _abi.H2SParams:
+        p = _abi.H2SParams()
+        p.transfer_in = _TRC_NAMES[self.transfer]
+        p.bits_in = self.bits_in
+        p.bits_out = self.bits_out
+        p.tonemap = _TM_NAMES[self.tonemapper.lower()]
+        p.tm_param = self.tm_param
+        p.desat = self.desat
+        p.peak = self.peak
+        p.npl = self.npl
+        p.gamma = self.gamma
+        p.maxcll = self.maxcll
+        p.mastering_max = self.mastering_max
+        p.lut_enabled = 1 if self.lut_enabled else 0
+        p.mode = _MODES[self.mode]
+        p.desat_luma = _DESAT_LUMA[self.desat_luma]
+        return p
+
+    # ---- back to the reference's chain string --------------------------
+    def filter_string(self, lut_path: str = '<LUT>') -> str:
+        """The CPU chain the reference would build for these params
+        (FFMPEG_CONVERT_FILTER.format, src/ffmpeg_command.py:246-247)."""
+        if is_gpu_only_tonemapper(self.tonemapper):
+            # src/ffmpeg_command.py:240-245
+            raise ValueError(f"{self.tonemapper.lower()} requires GPU tonemapping; the reference CPU chain "
+                             "has no equivalent")
+        return FFMPEG_CONVERT_FILTER.format(gamma=self.gamma, tonemapper=self.tonemapper.lower(),
+                                            lut_path=lut_path)
+
+
+_WRAP = re.compile(r'^\s*\[[^\]]*\](.*?)\[[^\]]*\]\s*$')
+
+
+def _split_filters(chain: str) -> 'list[tuple[str, dict[str, str], list[str]]]':
+    """Split 'name=a=1:b=2,name2=v' into (name, {key: value}, [positional])."""
+    out = []
+    for part in re.split(r',(?![^\[]*\])', chain):
+        part = part.strip()
+        if not part:
+            continue
+        name, _, args = part.partition('=')
+        kv: 'dict[str, str]' = {}
+        pos: 'list[str]' = []
+        # split on ':' not preceded by a backslash (escaped drive colons)
+        for tok in re.split(r'(?<!\\):', args) if args else []:
+            if '=' in tok:
+                k, _, v = tok.partition('=')
+                kv[k.strip()] = v.strip()
+            else:
+                pos.append(tok.strip())
+        out.append((name.strip(), kv, pos))
+    return out
+
+
+def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
+                       transfer: str = 'smpte2084', **overrides: Any) -> 'tuple[TonemapParams, str | None]':
+    """Parse a reference chain string into (params, lut_path).
+
+    Accepts FFMPEG_CONVERT_FILTER output (src/utils.py:38-42), the same
+    wrapped in build()'s '[0:v:0]...[vout]' (src/ffmpeg_command.py:480-483),
+    and the legacy no-LUT chain FFMPEG_FILTER_LEGACY_NO_LUT
+    (src/utils.py:57-60; its trailing scale= is a preview resize and is
+    rejected here).  Raises ValueError for anything outside the hot path."""
+    m = _WRAP.match(chain)
+    if m:
+        chain = m.group(1)
+    kw: 'dict[str, Any]' = dict(bits_in=bits_in, bits_out=bits_out, transfer=transfer,
+                                lut_enabled=False)
+    lut_path = None
+    seen_linear = False
+    for name, kv, pos in _split_filters(chain):
+        if name == 'zscale':
+            t = kv.get('t', kv.get('transfer'))
+            if t == 'linear':
+                seen_linear = True
+                if 'npl' in kv:
+                    kw['npl'] = float(kv['npl'])
+            elif t == 'bt709':
+                if not seen_linear:
+                    raise ValueError('zscale=t=bt709 before t=linear')
+                # p=bt709 here = the legacy closed-form gamut step
+            else:
+                raise ValueError(f'unsupported zscale stage {kv}')
+        elif name == 'tonemap':
+            tm = kv.get('tonemap', pos[0] if pos else None)
+            if tm is None:
+                raise ValueError('tonemap= without an operator')
+            kw['tonemapper'] = tm.lower()
+            if 'param' in kv:
+                kw['tm_param'] = float(kv['param'])
+            if 'desat' in kv:
+                kw['desat'] = float(kv['desat'])
+            if 'peak' in kv:
+                kw['peak'] = float(kv['peak'])
+        elif name == 'lut3d':
+            interp = kv.get('interp', 'tetrahedral')
+            if interp != 'tetrahedral':
+                raise ValueError(f'lut3d interp={interp} is not supported (reference uses tetrahedral)')
+            lut_path = kv.get('file', pos[0] if pos else None)
+            kw['lut_enabled'] = True
+        elif name == 'setparams':
+            continue  # metadata-only retag (src/utils.py:21-29)
+        elif name == 'eq':
+            if set(kv) - {'gamma'}:
+                raise ValueError(f'eq options other than gamma are not supported: {kv}')
+            kw['gamma'] = float(kv.get('gamma', 1.0))
+        else:
+            raise ValueError(f'filter {name!r} is outside the tone-mapping hot path')
+    if not seen_linear or 'tonemapper' not in kw:
+        raise ValueError('not a tone-mapping chain (needs zscale=t=linear and tonemap=)')
+    kw.update(overrides)
+    return TonemapParams(**kw), lut_path

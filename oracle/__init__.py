@@ -1,0 +1,233 @@
+"""Oracle — CPU restatement of the reference's hot path.
+
+TEST INFRASTRUCTURE.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this package, and only as the checker / CPU
+baseline.  The product (hdr-to-sdr_amd/hdr2sdr + libh2s) never imports, links
+or executes anything here.
+
+Contents
+* h2s_oracle.c (built to build/liboracle.so) — the per-pixel chain of
+  src/utils.py:38-42 restated stage by stage from the upstream algorithms
+  (zimg, vf_tonemap, vf_lut3d, vf_eq, swscale), see that file's header.
+* generate_cube_lines / convert — pure-Python restatement of
+  tools/generate_lut.py:36-109 (pinned: byte-identical to the reference's own
+  generator, sha256 in tests/golden/lut_hashes.json).
+* parse_cube — .cube text -> float32 the way lut3d reads it.
+
+Parity status: the LUT lattice is pinned exactly against the reference's
+generator.  The pixel stages S1-S8 live in ffmpeg N-125146-gc6bb22dea0 + zimg,
+which is absent from this container and not vendored: those stages are
+restatements of the published algorithms, pinned only by the reference's
+tests that do not need ffmpeg (argv goldens, LUT drift) — pixel parity against
+the real ffmpeg binary is UNPINNED (DESIGN.md "Oracle").
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'build', 'liboracle.so')
+
+
+class Params(ctypes.Structure):
+    """Layout of h2s_params (include/h2s.h)."""
+    _fields_ = [
+        ('transfer_in', ctypes.c_int32), ('bits_in', ctypes.c_int32),
+        ('bits_out', ctypes.c_int32), ('tonemap', ctypes.c_int32),
+        ('tm_param', ctypes.c_double), ('desat', ctypes.c_double),
+        ('peak', ctypes.c_double), ('npl', ctypes.c_double),
+        ('gamma', ctypes.c_double), ('maxcll', ctypes.c_double),
+        ('mastering_max', ctypes.c_double), ('lut_enabled', ctypes.c_int32),
+        ('mode', ctypes.c_int32), ('desat_luma', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 5),
+    ]
+
+
+class Frames(ctypes.Structure):
+    """Layout of h2s_frames (include/h2s.h)."""
+    _fields_ = [
+        ('data', ctypes.c_void_p * 3), ('linesize', ctypes.c_int64 * 3),
+        ('frame_pitch', ctypes.c_int64 * 3), ('width', ctypes.c_int32),
+        ('height', ctypes.c_int32), ('bits', ctypes.c_int32),
+        ('location', ctypes.c_int32),
+    ]
+
+
+def params_from(obj) -> Params:
+    """Copy same-named fields from any h2s_params-like object."""
+    p = Params()
+    for name, _ in Params._fields_:
+        if name == 'reserved':
+            continue
+        setattr(p, name, getattr(obj, name))
+    return p
+
+
+def default_params(**kw) -> Params:
+    """Reference chain defaults (see include/h2s.h h2s_params_default)."""
+    p = Params(transfer_in=0, bits_in=10, bits_out=10, tonemap=6, tm_param=math.nan,
+               desat=2.0, peak=0.0, npl=100.0, gamma=1.0, maxcll=0.0, mastering_max=0.0,
+               lut_enabled=1, mode=0, desat_luma=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f'{LIB_PATH} missing: run __graft_entry__.build()')
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_process.restype = ctypes.c_int
+        L.oracle_process.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.POINTER(Frames), ctypes.POINTER(Frames), ctypes.c_int,
+                                     ctypes.c_int]
+        L.oracle_debug_float.restype = ctypes.c_int
+        L.oracle_debug_float.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.POINTER(Frames), ctypes.c_int, ctypes.c_void_p]
+        L.oracle_resolved.restype = ctypes.c_int
+        L.oracle_resolved.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_int]
+        L.oracle_tone_curve.restype = ctypes.c_float
+        L.oracle_tone_curve.argtypes = [ctypes.POINTER(Params), ctypes.c_float]
+        L.oracle_pq_eotf.restype = ctypes.c_float
+        L.oracle_pq_eotf.argtypes = [ctypes.c_float]
+        L.oracle_hlg_inverse_oetf.restype = ctypes.c_float
+        L.oracle_hlg_inverse_oetf.argtypes = [ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def _frames(buf: np.ndarray, width: int, height: int, bits: int) -> Frames:
+    """Descriptor for a contiguous [F, W*H*3/2] host batch (hdr2sdr layout)."""
+    assert buf.flags['C_CONTIGUOUS']
+    sb = 1 if bits == 8 else 2
+    ysz = width * height * sb
+    csz = ysz // 4
+    d = Frames()
+    base = buf.ctypes.data
+    d.data[0], d.data[1], d.data[2] = base, base + ysz, base + ysz + csz
+    d.linesize[0] = width * sb
+    d.linesize[1] = d.linesize[2] = width // 2 * sb
+    for p in range(3):
+        d.frame_pitch[p] = ysz + 2 * csz
+    d.width, d.height, d.bits, d.location = width, height, bits, 1
+    return d
+
+
+def process(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
+            nthreads: int = 0) -> np.ndarray:
+    """Run the restated chain over a host batch; returns the output batch
+    (uint8 for bits_out 8, else uint16)."""
+    bits_in, bits_out = params.bits_in, params.bits_out
+    out = np.zeros((buf.shape[0], width * height * 3 // 2), dtype=np.uint8 if bits_out == 8 else np.uint16)
+    din = _frames(np.ascontiguousarray(buf), width, height, bits_in)
+    dout = _frames(out, width, height, bits_out)
+    lat, n = (None, 0)
+    if lattice is not None:
+        lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
+        n = round(lat.shape[0] ** (1 / 3))
+    rc = lib().oracle_process(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                              ctypes.byref(din), ctypes.byref(dout), buf.shape[0], nthreads)
+    if rc:
+        raise ValueError(f'oracle_process failed: {rc}')
+    return out
+
+
+def debug_float(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
+                stage: int) -> np.ndarray:
+    out = np.empty((3, height, width), dtype=np.float32)
+    din = _frames(np.ascontiguousarray(buf[:1]), width, height, params.bits_in)
+    lat, n = (None, 0)
+    if lattice is not None:
+        lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
+        n = round(lat.shape[0] ** (1 / 3))
+    rc = lib().oracle_debug_float(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                                  ctypes.byref(din), stage, out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_debug_float failed: {rc}')
+    return out
+
+
+def resolved(params: Params) -> 'tuple[float, float, np.ndarray]':
+    """(peak, param, eq_lut) after vf_tonemap / vf_eq initialisation."""
+    peak, param = ctypes.c_double(), ctypes.c_double()
+    eq = np.zeros(4096, dtype=np.uint16)
+    rc = lib().oracle_resolved(ctypes.byref(params), ctypes.byref(peak), ctypes.byref(param),
+                               eq.ctypes.data, eq.size)
+    if rc:
+        raise ValueError(f'oracle_resolved failed: {rc}')
+    q = params.bits_out if params.mode == 1 else 8
+    return peak.value, param.value, eq[:1 << q].copy()
+
+
+def tone_curve(params: Params, sig: float) -> float:
+    return float(lib().oracle_tone_curve(ctypes.byref(params), sig))
+
+
+def pq_eotf(x: float) -> float:
+    return float(lib().oracle_pq_eotf(x))
+
+
+def hlg_inverse_oetf(x: float) -> float:
+    return float(lib().oracle_hlg_inverse_oetf(x))
+
+
+# ---- tools/generate_lut.py restated (pure Python) --------------------------
+BT2020_TO_BT709 = [  # tools/generate_lut.py:36-40
+    [1.6604910021, -0.5876411388, -0.0728498633],
+    [-0.1245504745, 1.1328998971, -0.0083494226],
+    [-0.0181507634, -0.1005788980, 1.1187296614],
+]
+
+
+def convert(r: float, g: float, b: float) -> 'tuple[float, float, float]':
+    """tools/generate_lut.py:75-90: 2.4 decode, matrix, clamp, 1/2.4 encode."""
+    lin = [r ** 2.4, g ** 2.4, b ** 2.4]                         # :43-59
+    m = BT2020_TO_BT709
+    out = []
+    for row in m:
+        v = row[0] * lin[0] + row[1] * lin[1] + row[2] * lin[2]
+        v = max(0.0, min(1.0, v))                                # :71-72
+        out.append(v ** (1 / 2.4))                               # :62-68
+    return out[0], out[1], out[2]
+
+
+def generate_cube_lines(size: int) -> 'list[str]':
+    """tools/generate_lut.py:93-109: header + size^3 lines, red fastest."""
+    lines = [f'LUT_3D_SIZE {size}']
+    for bi in range(size):
+        b = bi / (size - 1)
+        for gi in range(size):
+            g = gi / (size - 1)
+            for ri in range(size):
+                r = ri / (size - 1)
+                o = convert(r, g, b)
+                lines.append(f'{o[0]:.6f} {o[1]:.6f} {o[2]:.6f}')
+    return lines
+
+
+def parse_cube(text: str) -> np.ndarray:
+    """lut3d's .cube read: data lines -> float32 [n^3, 3] (decimal -> double
+    -> float, as av_strtod + cast)."""
+    n = None
+    vals = []
+    for line in text.splitlines():
+        s = line.strip()
+        if not s or s.startswith('#') or s.startswith('TITLE') or s.startswith('DOMAIN_'):
+            continue
+        if s.startswith('LUT_3D_SIZE'):
+            n = int(s.split()[1])
+            continue
+        vals.append([float(t) for t in s.split()[:3]])
+    a = np.asarray(vals, dtype=np.float64).astype(np.float32)
+    assert n is not None and a.shape == (n ** 3, 3), (n, a.shape)
+    return a

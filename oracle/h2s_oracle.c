@@ -1,0 +1,576 @@
+/*
+ * h2s_oracle.c — CPU restatement of the reference's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this.  The product (libh2s) never
+ * links or calls it.
+ *
+ * What it restates
+ * ----------------
+ * The reference's hot path is the ffmpeg filtergraph
+ *   zscale=t=linear:npl=100,tonemap={tm},zscale=t=bt709:m=bt709:r=tv,
+ *   lut3d=file={lut}:interp=tetrahedral,setparams=...,eq=gamma={g}
+ * (src/utils.py:38-42) run on yuv420p10le/12le input and written to the
+ * -pix_fmt chosen by src/ffmpeg_command.py:355-360.  The arithmetic lives in
+ * FFmpeg N-125146-gc6bb22dea0 with zimg (THIRD_PARTY_NOTICES.md:10-17), which
+ * is absent from the container.  Each stage below restates the published
+ * upstream algorithm and names its source:
+ *   S1  zimg (vf_zscale): depth->float, bilinear chroma upsample (chroma
+ *       location "left", horizontal pass first), BT.2020-NCL Y'CbCr->R'G'B',
+ *       ST 2084 EOTF x 10000/npl, or ARIB B67 inverse OETF + OOTF x 1000/npl.
+ *   S2  libavfilter/vf_tonemap.c: desat, max(rgb), curve, rgb *= sig'/sig,
+ *       with the same float/double mix as the C source.
+ *   S3  zimg rec_1886_inverse_eotf: x < 0 ? 0 : x^(1/2.4) (the pure 2.4
+ *       gamma is pinned by tools/generate_lut.py:43-59).
+ *   S4  libavfilter/vf_lut3d.c: sanitizef, clip(x*(N-1)), interp_tetrahedral.
+ *   S6  swscale gbrpf32 -> yuv420p (auto-inserted before eq): modelled as
+ *       BT.709 limited-range matrix, centre-sited 2x2 box chroma,
+ *       round-half-up, no dither.  [EXT: model, not pinned]
+ *   S7  libavfilter/vf_eq.c create_lut (gamma only, Y plane only).
+ *   S8  swscale planarCopyWrapper 8 -> 10/12 bit: plain shift (tv range).
+ * Where a choice cannot be pinned without the bundled ffmpeg it is a named
+ * parameter (h2s_params.desat_luma, .mode) — see DESIGN.md "Oracle".
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/h2s.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef struct {
+  float r, g, b;
+} rgbf;
+
+/* ------------------------------------------------------------------------
+ * Resolved per-run constants (what vf_tonemap's init / filter_frame and
+ * zimg's graph builder compute once).                                      */
+typedef struct {
+  const h2s_params *p;
+  int q_bits;           /* quantisation depth: 8 (compat8) or bits_out   */
+  double peak;          /* vf_tonemap peak after ff_determine_signal_peak */
+  double param;         /* vf_tonemap param after init defaults           */
+  double desat;         /* 0 disables                                     */
+  double lr, lg, lb;    /* desat luma weights                             */
+  float y_scale, y_off, c_scale, c_off; /* zimg depth conversion          */
+  float m_rcr, m_gcb, m_gcr, m_bcb;      /* BT.2020-NCL YCbCr->RGB         */
+  float lin_scale;      /* 10000/npl (PQ) or 1000/npl (HLG)              */
+  /* BT.2390 */
+  double src_min, src_max, max_lum, ks;
+  uint16_t eq_lut[4096];
+  const float *lut;
+  int lut_n;
+} ocfg;
+
+/* ---- S1 helpers -------------------------------------------------------- */
+/* ST 2084 constants (exact in binary). */
+#define PQ_M1 0.1593017578125f
+#define PQ_M2 78.84375f
+#define PQ_C1 0.8359375f
+#define PQ_C2 18.8515625f
+#define PQ_C3 18.6875f
+
+/* zimg colorspace/gamma.cpp st_2084_eotf (normalised 1.0 = 10000 nits). */
+static float st2084_eotf(float x) {
+  if (x > 0.0f) {
+    float xpow = powf(x, 1.0f / PQ_M2);
+    float num = fmaxf(xpow - PQ_C1, 0.0f);
+    float den = fmaxf(PQ_C2 - PQ_C3 * xpow, FLT_MIN);
+    x = powf(num / den, 1.0f / PQ_M1);
+  } else {
+    x = 0.0f;
+  }
+  return x;
+}
+
+/* ARIB STD-B67 constants. */
+#define HLG_A 0.17883277f
+#define HLG_B 0.28466892f
+#define HLG_C 0.55991073f
+
+/* zimg arib_b67_inverse_oetf. */
+static float arib_b67_inverse_oetf(float x) {
+  x = fmaxf(x, 0.0f);
+  if (x <= 0.5f)
+    x = (x * x) * (1.0f / 3.0f);
+  else
+    x = (expf((x - HLG_C) / HLG_A) + HLG_B) * (1.0f / 12.0f);
+  return x;
+}
+
+/* ---- S2: libavfilter/vf_tonemap.c -------------------------------------- */
+static float hable(float in) {
+  float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
+  return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
+}
+
+static float mobius(float in, float j, double peak) {
+  float a, b;
+  if (in <= j) return in;
+  a = -j * j * (peak - 1.0f) / (j * j - 2.0f * j + peak);
+  b = (j * j - 2.0f * j * peak + peak) / fmax(peak - 1.0f, 1e-6);
+  return (b * b + 2.0f * b * j + j * j) / (b - a) * (in + a) / (in + b);
+}
+
+/* ST 2084 inverse EOTF (for BT.2390's PQ-domain EETF), double precision. */
+static double pq_encode_d(double y) {
+  double ym = pow(fmax(y, 0.0), (double)PQ_M1);
+  return pow((PQ_C1 + PQ_C2 * ym) / (1.0 + PQ_C3 * ym), (double)PQ_M2);
+}
+
+static float pq_encode_f(float y) {
+  float ym = powf(fmaxf(y, 0.0f), PQ_M1);
+  return powf((PQ_C1 + PQ_C2 * ym) / (1.0f + PQ_C3 * ym), PQ_M2);
+}
+
+/* BT.2390-8 section 5.4 EETF on the PQ-encoded signal (Lmin = Lb = 0).  The
+ * reference reaches BT.2390 only through libplacebo (src/utils.py:62-73,
+ * :445-449); that implementation is not restated here: parity unpinned. */
+static float bt2390_sig(const ocfg *c, float sig) {
+  float e1 = pq_encode_f(sig * (float)(c->p->npl / 10000.0));
+  float e1n = (e1 - (float)c->src_min) / (float)(c->src_max - c->src_min);
+  float ks = (float)c->ks, ml = (float)c->max_lum;
+  float e2 = e1n;
+  if (ks < 1.0f && e1n > ks) {
+    float t = (e1n - ks) / (1.0f - ks);
+    float t2 = t * t, t3 = t2 * t;
+    e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * ks + (t3 - 2.0f * t2 + t) * (1.0f - ks) +
+         (-2.0f * t3 + 3.0f * t2) * ml;
+  }
+  float e4 = e2 * (float)(c->src_max - c->src_min) + (float)c->src_min;
+  /* back to linear, in units of npl */
+  return st2084_eotf(e4) * (float)(10000.0 / c->p->npl);
+}
+
+#define MIX(x, y, a) (x) * (1 - (a)) + (y) * (a)
+
+static rgbf tonemap_px(const ocfg *c, rgbf in) {
+  rgbf o = in;
+  float sig, sig_orig;
+  int tm = c->p->tonemap;
+  if (tm == H2S_TM_BT2390) {
+    sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
+    float s2 = bt2390_sig(c, sig);
+    o.r *= s2 / sig;
+    o.g *= s2 / sig;
+    o.b *= s2 / sig;
+    return o;
+  }
+  if (c->desat > 0) {
+    float luma = c->lr * in.r + c->lg * in.g + c->lb * in.b;
+    float overbright = fmax(luma - c->desat, 1e-6) / fmax(luma, 1e-6);
+    o.r = MIX(in.r, luma, overbright);
+    o.g = MIX(in.g, luma, overbright);
+    o.b = MIX(in.b, luma, overbright);
+  }
+  {
+    float m = o.r > o.g ? o.r : o.g;
+    m = m > o.b ? m : o.b;
+    sig = m > 1e-6 ? m : (float)1e-6;
+  }
+  sig_orig = sig;
+  double peak = c->peak, param = c->param;
+  switch (tm) {
+    default:
+    case H2S_TM_NONE:
+      break;
+    case H2S_TM_LINEAR:
+      sig = sig * param / peak;
+      break;
+    case H2S_TM_GAMMA:
+      sig = sig > 0.05f ? pow(sig / peak, 1.0f / param)
+                        : sig * pow(0.05f / peak, 1.0f / param) / 0.05f;
+      break;
+    case H2S_TM_CLIP: {
+      float v = sig * param;
+      sig = v < 0 ? 0 : (v > 1.0f ? 1.0f : v);
+      break;
+    }
+    case H2S_TM_HABLE:
+      sig = hable(sig) / hable((float)peak);
+      break;
+    case H2S_TM_REINHARD:
+      sig = sig / (sig + param) * (peak + param) / peak;
+      break;
+    case H2S_TM_MOBIUS:
+      sig = mobius(sig, (float)param, peak);
+      break;
+  }
+  o.r *= sig / sig_orig;
+  o.g *= sig / sig_orig;
+  o.b *= sig / sig_orig;
+  return o;
+}
+
+/* ---- S3: zimg rec_1886_inverse_eotf ------------------------------------ */
+static float bt1886_inverse(float x) { return x < 0.0f ? 0.0f : powf(x, 1.0f / 2.4f); }
+
+/* ---- S4: libavfilter/vf_lut3d.c ---------------------------------------- */
+static float sanitizef(float f) {
+  union {
+    float f;
+    uint32_t i;
+  } t;
+  t.f = f;
+  if ((t.i & 0x7f800000u) == 0x7f800000u) {
+    if (t.i & 0x007fffffu) return 0.0f;
+    if (t.i & 0x80000000u) return -FLT_MAX;
+    return FLT_MAX;
+  }
+  return f;
+}
+
+static float clipf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* lattice point (ri, gi, bi) in .cube order (red fastest). */
+static rgbf lat(const ocfg *c, int ri, int gi, int bi) {
+  const float *e = c->lut + 3 * (((size_t)bi * c->lut_n + gi) * c->lut_n + ri);
+  rgbf v = {e[0], e[1], e[2]};
+  return v;
+}
+
+static rgbf lut3d_tetra(const ocfg *c, rgbf in) {
+  const float lut_max = (float)(c->lut_n - 1);
+  const float sr = 1.0f * lut_max, sg = 1.0f * lut_max, sb = 1.0f * lut_max;
+  rgbf s = {clipf(sanitizef(in.r) * sr, 0, lut_max), clipf(sanitizef(in.g) * sg, 0, lut_max),
+            clipf(sanitizef(in.b) * sb, 0, lut_max)};
+  int n = c->lut_n;
+  int pr = (int)s.r, pg = (int)s.g, pb = (int)s.b;
+  int nr = pr + 1 < n - 1 ? pr + 1 : n - 1;
+  int ng = pg + 1 < n - 1 ? pg + 1 : n - 1;
+  int nb = pb + 1 < n - 1 ? pb + 1 : n - 1;
+  rgbf d = {s.r - pr, s.g - pg, s.b - pb};
+  rgbf c000 = lat(c, pr, pg, pb), c111 = lat(c, nr, ng, nb), o;
+#define TET(w0, A, w1, B, w2, w3)                                            \
+  do {                                                                       \
+    o.r = (w0) * c000.r + (w1) * A.r + (w2) * B.r + (w3) * c111.r;           \
+    o.g = (w0) * c000.g + (w1) * A.g + (w2) * B.g + (w3) * c111.g;           \
+    o.b = (w0) * c000.b + (w1) * A.b + (w2) * B.b + (w3) * c111.b;           \
+  } while (0)
+  if (d.r > d.g) {
+    if (d.g > d.b) {
+      rgbf c100 = lat(c, nr, pg, pb), c110 = lat(c, nr, ng, pb);
+      TET(1 - d.r, c100, d.r - d.g, c110, d.g - d.b, d.b);
+    } else if (d.r > d.b) {
+      rgbf c100 = lat(c, nr, pg, pb), c101 = lat(c, nr, pg, nb);
+      TET(1 - d.r, c100, d.r - d.b, c101, d.b - d.g, d.g);
+    } else {
+      rgbf c001 = lat(c, pr, pg, nb), c101 = lat(c, nr, pg, nb);
+      TET(1 - d.b, c001, d.b - d.r, c101, d.r - d.g, d.g);
+    }
+  } else {
+    if (d.b > d.g) {
+      rgbf c001 = lat(c, pr, pg, nb), c011 = lat(c, pr, ng, nb);
+      TET(1 - d.b, c001, d.b - d.g, c011, d.g - d.r, d.r);
+    } else if (d.b > d.r) {
+      rgbf c010 = lat(c, pr, ng, pb), c011 = lat(c, pr, ng, nb);
+      TET(1 - d.g, c010, d.g - d.b, c011, d.b - d.r, d.r);
+    } else {
+      rgbf c010 = lat(c, pr, ng, pb), c110 = lat(c, nr, ng, pb);
+      TET(1 - d.g, c010, d.g - d.r, c110, d.r - d.b, d.b);
+    }
+  }
+#undef TET
+  return o;
+}
+
+/* lut_enabled = 0: the legacy closed-form gamut step
+ * (FFMPEG_FILTER_LEGACY_NO_LUT, src/utils.py:57-60: zscale ...:p=bt709),
+ * i.e. linear BT.2020 -> BT.709 matrix (tools/generate_lut.py:36-40), then
+ * BT.1886 inverse; out-of-range values clip at the [0,1] swscale input. */
+static const float M2020_709[3][3] = {{1.6604910021f, -0.5876411388f, -0.0728498633f},
+                                      {-0.1245504745f, 1.1328998971f, -0.0083494226f},
+                                      {-0.0181507634f, -0.1005788980f, 1.1187296614f}};
+
+/* ---- one pixel through S1(after upsample)..S4 --------------------------- */
+static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf *dbg) {
+  (void)dbg;
+  rgbf e;
+  e.r = y + c->m_rcr * cr;
+  e.g = y + c->m_gcb * cb + c->m_gcr * cr;
+  e.b = y + c->m_bcb * cb;
+  rgbf l;
+  if (c->p->transfer_in == H2S_TRC_HLG) {
+    l.r = arib_b67_inverse_oetf(e.r);
+    l.g = arib_b67_inverse_oetf(e.g);
+    l.b = arib_b67_inverse_oetf(e.b);
+    float ys = 0.2627f * l.r + 0.6780f * l.g + 0.0593f * l.b;
+    float w = ys > 0.0f ? c->lin_scale * powf(ys, 0.2f) : 0.0f;
+    l.r *= w;
+    l.g *= w;
+    l.b *= w;
+  } else {
+    l.r = st2084_eotf(e.r) * c->lin_scale;
+    l.g = st2084_eotf(e.g) * c->lin_scale;
+    l.b = st2084_eotf(e.b) * c->lin_scale;
+  }
+  if (upto == H2S_STAGE_LINEAR) return l;
+  rgbf t = tonemap_px(c, l);
+  if (upto == H2S_STAGE_TONEMAP) return t;
+  rgbf g;
+  if (c->p->lut_enabled) {
+    g.r = bt1886_inverse(t.r);
+    g.g = bt1886_inverse(t.g);
+    g.b = bt1886_inverse(t.b);
+    if (upto == H2S_STAGE_GAMMA) return g;
+    return lut3d_tetra(c, g);
+  }
+  rgbf m;
+  m.r = M2020_709[0][0] * t.r + M2020_709[0][1] * t.g + M2020_709[0][2] * t.b;
+  m.g = M2020_709[1][0] * t.r + M2020_709[1][1] * t.g + M2020_709[1][2] * t.b;
+  m.b = M2020_709[2][0] * t.r + M2020_709[2][1] * t.g + M2020_709[2][2] * t.b;
+  g.r = clipf(bt1886_inverse(m.r), 0.0f, 1.0f);
+  g.g = clipf(bt1886_inverse(m.g), 0.0f, 1.0f);
+  g.b = clipf(bt1886_inverse(m.b), 0.0f, 1.0f);
+  return g;
+}
+
+/* ---- configuration ------------------------------------------------------ */
+static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
+  memset(c, 0, sizeof(*c));
+  c->p = p;
+  c->lut = lut;
+  c->lut_n = n;
+  if (p->bits_in != 10 && p->bits_in != 12) return H2S_E_UNSUPPORTED;
+  if (p->bits_out != 8 && p->bits_out != 10 && p->bits_out != 12) return H2S_E_UNSUPPORTED;
+  c->q_bits = p->mode == H2S_MODE_NATIVE ? p->bits_out : 8;
+
+  /* vf_tonemap init: parameter defaults */
+  double param = p->tm_param;
+  switch (p->tonemap) {
+    case H2S_TM_GAMMA:
+      if (isnan(param)) param = 1.8;
+      break;
+    case H2S_TM_REINHARD:
+      if (!isnan(param)) param = (1.0 - param) / param;
+      break;
+    case H2S_TM_MOBIUS:
+      if (isnan(param)) param = 0.3;
+      break;
+  }
+  if (isnan(param)) param = 1.0;
+  c->param = param;
+  /* ff_determine_signal_peak (libavfilter/colorspace.c): MaxCLL, then
+   * mastering max, then trc default; the trc seen by tonemap is linear
+   * (zscale t=linear set it), so the default is 10.0. REFERENCE_WHITE=100 */
+  double peak = p->peak;
+  if (!(peak > 0)) {
+    peak = 0;
+    if (p->maxcll > 0) peak = p->maxcll / 100.0;
+    if (!(peak > 0) && p->mastering_max > 0) peak = p->mastering_max / 100.0;
+    if (!(peak > 0)) peak = 10.0;
+  }
+  c->peak = peak;
+  c->desat = p->desat;
+  switch (p->desat_luma) {
+    case H2S_DESAT_LUMA_BT2020:
+      c->lr = 0.2627, c->lg = 0.6780, c->lb = 0.0593;
+      break;
+    case H2S_DESAT_LUMA_BT709:
+      c->lr = 0.2126, c->lg = 0.7152, c->lb = 0.0722;
+      break;
+    default:
+      c->lr = 1, c->lg = 1, c->lb = 1;
+  }
+
+  /* zimg depth conversion (limited range): x * (1/range) - offset/range */
+  int sh = p->bits_in - 8;
+  c->y_scale = (float)(1.0 / (219 << sh));
+  c->y_off = (float)(-(double)(16 << sh) / (219 << sh));
+  c->c_scale = (float)(1.0 / (224 << sh));
+  c->c_off = (float)(-(double)(128 << sh) / (224 << sh));
+  /* BT.2020-NCL Y'CbCr -> R'G'B' */
+  const double kr = 0.2627, kb = 0.0593, kg = 1.0 - kr - kb;
+  c->m_rcr = (float)(2.0 * (1.0 - kr));
+  c->m_gcb = (float)(-2.0 * kb * (1.0 - kb) / kg);
+  c->m_gcr = (float)(-2.0 * kr * (1.0 - kr) / kg);
+  c->m_bcb = (float)(2.0 * (1.0 - kb));
+  c->lin_scale = (float)((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl);
+
+  /* BT.2390 constants: source [0, peak*100 nits], target [0, npl nits] */
+  c->src_min = pq_encode_d(0.0);
+  c->src_max = pq_encode_d(peak * 100.0 / 10000.0);
+  c->max_lum = (pq_encode_d(p->npl / 10000.0) - c->src_min) / (c->src_max - c->src_min);
+  c->ks = 1.5 * c->max_lum - 0.5;
+
+  /* vf_eq create_lut (gamma only; contrast 1, brightness 0, weight 1),
+   * generalised to 2^q entries for native mode. */
+  int qn = 1 << c->q_bits, qmax = qn - 1;
+  double g = 1.0 / p->gamma;
+  for (int i = 0; i < qn; i++) {
+    double v = i / (double)qmax;
+    v = 1.0 * (v - 0.5) + 0.5 + 0.0;
+    if (v <= 0.0) {
+      c->eq_lut[i] = 0;
+    } else {
+      v = v * 0.0 + pow(v, g) * 1.0;
+      if (v >= 1.0)
+        c->eq_lut[i] = (uint16_t)qmax;
+      else
+        c->eq_lut[i] = (uint16_t)(int)((double)qn * v);
+    }
+  }
+  if (p->lut_enabled && (!lut || n < 2)) return H2S_E_LUT_MISSING;
+  return 0;
+}
+
+/* ---- sample access ------------------------------------------------------- */
+static inline int rd(const h2s_frames *f, int plane, int frame, int x, int y) {
+  const uint8_t *row =
+      (const uint8_t *)f->data[plane] + (int64_t)frame * f->frame_pitch[plane] + (int64_t)y * f->linesize[plane];
+  if (f->bits == 8) return row[x];
+  uint16_t v;
+  memcpy(&v, row + 2 * x, 2);
+  return v;
+}
+
+static inline void wr(const h2s_frames *f, int plane, int frame, int x, int y, int v) {
+  uint8_t *row = (uint8_t *)f->data[plane] + (int64_t)frame * f->frame_pitch[plane] + (int64_t)y * f->linesize[plane];
+  if (f->bits == 8) {
+    row[x] = (uint8_t)v;
+  } else {
+    uint16_t w = (uint16_t)v;
+    memcpy(row + 2 * x, &w, 2);
+  }
+}
+
+/* zimg resize edge rule for the 2-tap bilinear kernel: position -1 mirrors
+ * to 1, position n folds to n-1 (zimg resize/filter.cpp compute_filter). */
+static inline int edge(int i, int n) {
+  if (i < 0) i = -i;
+  if (i > n - 1) i = n - 1;
+  return i;
+}
+
+/* normalised chroma sample */
+static inline float csamp(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
+  return (float)rd(in, plane, frame, edge(x, cw), edge(y, ch)) * c->c_scale + c->c_off;
+}
+
+/* horizontal pass (left siting): luma column x from chroma row cy */
+static inline float hpass(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int cy, int cw, int ch) {
+  int k = x >> 1;
+  if (!(x & 1)) return csamp(c, in, plane, frame, k, cy, cw, ch);
+  return 0.5f * csamp(c, in, plane, frame, k, cy, cw, ch) + 0.5f * csamp(c, in, plane, frame, k + 1, cy, cw, ch);
+}
+
+/* vertical pass (centre siting): luma row y */
+static inline float upsample(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
+  int m = y >> 1;
+  if (!(y & 1))
+    return 0.25f * hpass(c, in, plane, frame, x, m - 1, cw, ch) + 0.75f * hpass(c, in, plane, frame, x, m, cw, ch);
+  return 0.75f * hpass(c, in, plane, frame, x, m, cw, ch) + 0.25f * hpass(c, in, plane, frame, x, m + 1, cw, ch);
+}
+
+/* ---- S6 model + S7 + S8 -------------------------------------------------- */
+static const float K709_R = 0.2126f, K709_G = 0.7152f, K709_B = 0.0722f;
+
+static inline int quant(float v, int qmax) {
+  int i = (int)floorf(v + 0.5f);
+  return i < 0 ? 0 : (i > qmax ? qmax : i);
+}
+
+static void process_quad_row(const ocfg *c, const h2s_frames *in, const h2s_frames *out, int f, int cy) {
+  const h2s_params *p = c->p;
+  int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
+  int q = c->q_bits, qmax = (1 << q) - 1;
+  float s = (float)(1 << (q - 8));
+  int shift_out = p->mode == H2S_MODE_NATIVE ? 0 : p->bits_out - 8;
+  const float cbr = (float)(-0.2126 / 1.8556), cbg = (float)(-0.7152 / 1.8556), cbb = (float)(0.9278 / 1.8556);
+  const float crr = (float)(0.7874 / 1.5748), crg = (float)(-0.7152 / 1.5748), crb = (float)(-0.0722 / 1.5748);
+  for (int cx = 0; cx < cw; cx++) {
+    float cbs[4], crs[4];
+    for (int k = 0; k < 4; k++) {
+      int x = 2 * cx + (k & 1), y = 2 * cy + (k >> 1);
+      float yv = (float)rd(in, 0, f, x, y) * c->y_scale + c->y_off;
+      float cb = upsample(c, in, 1, f, x, y, cw, ch);
+      float cr = upsample(c, in, 2, f, x, y, cw, ch);
+      rgbf o = chain_px(c, yv, cb, cr, 99, NULL);
+      float R = clipf(o.r, 0.0f, 1.0f), G = clipf(o.g, 0.0f, 1.0f), B = clipf(o.b, 0.0f, 1.0f);
+      float Y = K709_R * R + K709_G * G + K709_B * B;
+      cbs[k] = cbr * R + cbg * G + cbb * B;
+      crs[k] = crr * R + crg * G + crb * B;
+      int yq = quant((16.0f + 219.0f * Y) * s, qmax);
+      wr(out, 0, f, x, y, (int)c->eq_lut[yq] << shift_out);
+    }
+    float cb = ((cbs[0] + cbs[1]) + (cbs[2] + cbs[3])) * 0.25f;
+    float cr = ((crs[0] + crs[1]) + (crs[2] + crs[3])) * 0.25f;
+    wr(out, 1, f, cx, cy, quant((128.0f + 224.0f * cb) * s, qmax) << shift_out);
+    wr(out, 2, f, cx, cy, quant((128.0f + 224.0f * cr) * s, qmax) << shift_out);
+  }
+}
+
+/* ---- exported entry points (ctypes) ------------------------------------- */
+int oracle_process(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in,
+                   const h2s_frames *out, int nframes, int nthreads) {
+  ocfg c;
+  int rc = resolve(&c, p, lut, lut_n);
+  if (rc) return rc;
+  if (in->width != out->width || in->height != out->height || (in->width & 1) || (in->height & 1) ||
+      in->bits != p->bits_in || out->bits != p->bits_out)
+    return H2S_E_INVALID_ARG;
+  int ch = in->height / 2;
+  int64_t rows = (int64_t)nframes * ch;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t r = 0; r < rows; r++) process_quad_row(&c, in, out, (int)(r / ch), (int)(r % ch));
+  (void)nthreads;
+  return 0;
+}
+
+/* float RGB (planar) of frame 0 after `stage` */
+int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, int stage,
+                       float *out_rgb) {
+  ocfg c;
+  int rc = resolve(&c, p, lut, lut_n);
+  if (rc) return rc;
+  int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
+  size_t plane = (size_t)W * H;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      float yv = (float)rd(in, 0, 0, x, y) * c.y_scale + c.y_off;
+      float cb = upsample(&c, in, 1, 0, x, y, cw, ch);
+      float cr = upsample(&c, in, 2, 0, x, y, cw, ch);
+      rgbf o = chain_px(&c, yv, cb, cr, stage, NULL);
+      size_t i = (size_t)y * W + x;
+      out_rgb[i] = o.r;
+      out_rgb[plane + i] = o.g;
+      out_rgb[2 * plane + i] = o.b;
+    }
+  return 0;
+}
+
+/* resolved constants, for tests of the parameter logic */
+int oracle_resolved(const h2s_params *p, double *peak, double *param, uint16_t *eq_lut, int eq_cap) {
+  ocfg c;
+  int rc = resolve(&c, p, NULL, 0);
+  if (rc && rc != H2S_E_LUT_MISSING) return rc;
+  if (peak) *peak = c.peak;
+  if (param) *param = c.param;
+  int qn = 1 << c.q_bits;
+  for (int i = 0; i < qn && i < eq_cap; i++) eq_lut[i] = c.eq_lut[i];
+  return 0;
+}
+
+/* single-pixel tone-curve probe: sig -> sig' (for known-answer tests) */
+float oracle_tone_curve(const h2s_params *p, float sig) {
+  ocfg c;
+  resolve(&c, p, NULL, 0);
+  h2s_params q = *p;
+  q.desat = 0;
+  c.p = &q;
+  c.desat = 0;
+  rgbf in = {sig, sig, sig};
+  rgbf o = tonemap_px(&c, in);
+  return o.r;
+}
+
+float oracle_pq_eotf(float x) { return st2084_eotf(x); }
+float oracle_hlg_inverse_oetf(float x) { return arib_b67_inverse_oetf(x); }
