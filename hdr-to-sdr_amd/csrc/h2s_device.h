@@ -50,6 +50,50 @@ struct KParams {
   const uint16_t* eq_lut;
   // Y'CbCr 709 rows
   float k709[3], kcb[3], kcr[3];
+  int gx0;  // first column group this launch covers (tail launches)
+};
+
+// Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
+// with every scale folded into constants.
+struct FastParams {
+  int W, H, cw, ch;                // luma / chroma geometry (W % 64 == 0)
+  unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
+  const uint8_t* in[3];
+  long long in_ls[3], in_fp[3];
+  uint8_t* out[3];
+  long long out_ls[3], out_fp[3];
+  // S1: R'G'B' = k + ys*Y + a*{U,V}; index [0] even columns (x4), [1] odd (x8)
+  float ys, k_r, k_g, k_b;
+  float a_rv[2], a_gv[2], a_gu[2], a_bu[2];
+  float log2_lin_scale;
+  // S2
+  float lr, lg, lb, desat;
+  float rein_p, rein_k;
+  float hable_peak_inv, hable_ef_peak_inv;
+  float mob_j, mob_a, mob_b, mob_k;
+  float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
+  // S3/S4: lattice coordinates and byte offsets (float4 records)
+  float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
+  float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)
+  int og, ob, cr, cg, cb, c111;                // corner byte offsets
+  const float* lut_yuv;                        // 12-byte records (Y', Cb', Cr')
+  int lut_bytes;
+  // S6..S8
+  const uint16_t* eq_lut;
+  int eq_n;
+  float c_bias;
+  int shift_out, out8;
+  // S1 PQ EOTF (x 10000/npl) as a piecewise cubic: segment i covers
+  // E in [i, i+1)/PQ_SEG, coefficients (c3, c2, c1, c0) of t = E*PQ_SEG - i
+  const float4* pq_tab;
+};
+
+constexpr int PQ_SEG = 128;          // segments per unit of E
+constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
+constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
+
+struct YuvLutConsts {
+  float s, k709[3], kcb[3], kcr[3];
 };
 
 // ---- fast transcendentals (v_log_f32 / v_exp_f32 / v_rcp_f32) ----------
@@ -104,6 +148,7 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
   if (P.tonemap == 7 /* BT2390 */) {
     sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     float e1n = (pq_encode(sig * P.npl_1e4) - P.b_srcmin) * P.b_inv_range;
+    e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);  // clip to the source range (NaN -> 1)
     float e2 = e1n;
     if (P.b_ks < 1.0f && e1n > P.b_ks) {
       float t = (e1n - P.b_ks) * P.b_inv_1mks;

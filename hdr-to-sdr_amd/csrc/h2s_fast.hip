@@ -1,0 +1,418 @@
+// h2s_fast.hip — specialised fast path of the fused tone-map kernel.
+//
+// Same chain as k_generic (h2s_kernels.hip) and oracle/h2s_oracle.c, restated
+// for throughput on gfx950:
+//  * one template instance per (transfer, operator, desat) so the 16 pixels a
+//    work item owns are straight-line code the compiler can interleave (the
+//    v1 kernel's per-pixel uniform branches serialised every LUT gather);
+//  * chroma upsampling on integer-valued floats (exact), the 1/4, 1/8 and
+//    depth-normalisation scales folded into the Y'CbCr->R'G'B' constants;
+//  * the 3D-LUT lattice pre-multiplied into output Y'CbCr code space
+//    (RGB->Y'CbCr is linear and the lattice lies in [0,1], so the swscale
+//    clip is a no-op and blend-then-convert == convert-then-blend); the
+//    tetrahedral blend then yields quantiser inputs directly;
+//  * lattice gathers are buffer loads (32-bit offsets, one SGPR base);
+//  * eq's table sits in LDS.
+// Geometry (k_tile): a block of 256 threads owns a 64 x 32 luma tile of one
+// frame.  The tile (Y, and U/V with their 1-sample halo) is staged into LDS
+// with coalesced 16-byte loads; then, in 8 steps, each wave processes one
+// dense 8 x 8 pixel sub-block with one pixel per lane (lanes 4q..4q+3 = one
+// 2x2 quad).  Dense sub-blocks keep the 64 lanes of every lattice gather on
+// few cache lines (the gathers, not the arithmetic, bound this kernel);
+// chroma is reduced per quad with DPP quad permutes and all outputs leave
+// through LDS as 16-byte coalesced stores.
+#include <hip/hip_runtime.h>
+
+#include "h2s_device.h"
+
+namespace h2s {
+
+typedef float f3 __attribute__((ext_vector_type(3)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+// streaming frame I/O: non-temporal so the pixels do not evict LUT lines
+__device__ __forceinline__ uint2 nt_ld2(const uint8_t* p) {
+  const u2v v = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p));
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 nt_ld4(const uint8_t* p) {
+  const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_st2(uint2 w, uint8_t* p) {
+  __builtin_nontemporal_store(u2v{w.x, w.y}, reinterpret_cast<u2v*>(p));
+}
+__device__ __forceinline__ void nt_st4(uint4 w, uint8_t* p) {
+  __builtin_nontemporal_store(u4v{w.x, w.y, w.z, w.w}, reinterpret_cast<u4v*>(p));
+}
+
+__device__ __forceinline__ int fedge(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i > n - 1 ? n - 1 : i;
+}
+
+__device__ __forceinline__ long long fxcd_remap(long long b, long long nb) {
+  const long long xcd = b & 7, idx = b >> 3, per = nb >> 3, rem = nb & 7;
+  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
+// exact zimg st_2084_eotf x 10000/npl (used above the table's range)
+__device__ __forceinline__ float pq_exact(const FastParams& F, float e) {
+  const float xp = fexp2(flog2(fmaxf(e, 0.0f)) * (1.0f / PQ_M2));
+  const float num = fmaxf(xp - PQ_C1, 0.0f);
+  const float den = fmaxf(PQ_C2 - PQ_C3 * xp, 1.17549435e-38f);  // zimg: max(.., FLT_MIN)
+  return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + F.log2_lin_scale);
+}
+
+// table form: 4 full-rate VALU + 2 half-rate + one LDS read, no transcendentals
+__device__ __forceinline__ float pq_table(const float4* tab, float e) {
+  const float u = __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * 0.99999994f) * (float)PQ_SEG;
+  const float4 c = tab[(int)u];
+  const float t = __builtin_amdgcn_fractf(u);
+  return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
+}
+
+// S1 transfer to linear (units of npl), specialised
+template <int TRC>
+__device__ __forceinline__ void to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
+                                          float& r, float& g, float& b) {
+  if (TRC == 0) {
+    r = pq_table(pq_lds, er), g = pq_table(pq_lds, eg), b = pq_table(pq_lds, eb);
+    const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
+    if (__builtin_amdgcn_ballot_w64(emax >= PQ_EMAX)) {  // rare: extreme out-of-gamut codes
+      r = er >= PQ_EMAX ? pq_exact(F, er) : r;
+      g = eg >= PQ_EMAX ? pq_exact(F, eg) : g;
+      b = eb >= PQ_EMAX ? pq_exact(F, eb) : b;
+    }
+  } else {
+    // zimg arib_b67_inverse_oetf, branch-free; then the OOTF (gamma 1.2)
+    auto inv = [](float e) -> float {
+      const float x = fmaxf(e, 0.0f);
+      const float lo = (x * x) * (1.0f / 3.0f);
+      const float hi = (fexp2((x - HLG_C) * (1.4426950408889634f / HLG_A)) + HLG_B) * (1.0f / 12.0f);
+      return x <= 0.5f ? lo : hi;
+    };
+    r = inv(er), g = inv(eg), b = inv(eb);
+    const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
+    const float w = fexp2(flog2(ys) * 0.2f + F.log2_lin_scale);  // ys == 0 -> 0
+    r *= w, g *= w, b *= w;
+  }
+}
+
+// S2 vf_tonemap, specialised; returns the gain k = sig'/sig applied to rgb
+template <int TM, bool DESAT>
+__device__ __forceinline__ void tone(const FastParams& F, float& r, float& g, float& b) {
+  if (TM == 7) {  // BT.2390 (no desat), branch-free PQ encode / decode
+    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
+    const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
+    const float e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
+    const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
+    float e2 = e1n;
+    const float t = (e1n - F.b_ks) * F.b_inv_1mks;
+    const float t2 = t * t, t3 = t2 * t;
+    const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
+                    (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
+    e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
+    const float e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);
+    const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
+    const float s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
+    const float k = s2 * frcp(sig);
+    r *= k, g *= k, b *= k;
+    return;
+  }
+  if (DESAT) {
+    const float luma = F.lr * r + F.lg * g + F.lb * b;
+    const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
+    const float iob = 1.0f - ob;
+    r = r * iob + luma * ob;
+    g = g * iob + luma * ob;
+    b = b * iob + luma * ob;
+  }
+  const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
+  // gain k = curve(sig) / sig with one reciprocal
+  float k;
+  if (TM == 4) {  // REINHARD: sig/(sig+p) * (peak+p)/peak
+    k = F.rein_k * frcp(sig + F.rein_p);
+  } else if (TM == 5) {  // HABLE: hable(sig) / hable(peak); two reciprocals keep
+    // huge (out-of-range) sig from overflowing den * sig
+    const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
+    const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
+    k = fmaf(num * frcp(den), F.hable_peak_inv, -F.hable_ef_peak_inv) * frcp(sig);
+  } else {  // MOBIUS: identity below j
+    const float m = F.mob_k * (sig + F.mob_a) * frcp(sig + F.mob_b) * frcp(sig);
+    k = sig <= F.mob_j ? 1.0f : m;
+  }
+  r *= k, g *= k, b *= k;
+}
+
+// S3 + S4 coordinates: s = clamp((N-1) * x^(1/2.4)), as lattice units
+// NaN -> 0 (lut3d sanitizef), +inf -> top of the lattice
+__device__ __forceinline__ float lut_s(const FastParams& F, float x) {
+  return fminf(fmaxf(fexp2(flog2(x) * (1.0f / 2.4f) + F.log2_nm1), 0.0f), F.s_max);
+}
+
+
+constexpr int TBW = 64, TBH = 32;  // luma tile of one block
+constexpr int CBW = 32, CBH = 16;  // chroma tile
+constexpr int YST = 68;            // LDS row stride (floats) of the luma tile
+constexpr int HST = 68;            // LDS row stride of the horizontally upsampled chroma rows
+constexpr int NT = 2;              // buffer-op aux bits: non-temporal (streamed frame bytes)
+
+__device__ __forceinline__ float pair_sum(float v) {
+  // v0 + v1 in both lanes of each horizontal pixel pair of a quad
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ void unpack8(const uint4 a, float* o) {
+  o[0] = (float)(a.x & 0xffff), o[1] = (float)(a.x >> 16), o[2] = (float)(a.y & 0xffff), o[3] = (float)(a.y >> 16);
+  o[4] = (float)(a.z & 0xffff), o[5] = (float)(a.z >> 16), o[6] = (float)(a.w & 0xffff), o[7] = (float)(a.w >> 16);
+}
+
+// keep a wave-uniform constant in a VGPR (avoids per-use SGPR->VGPR moves
+// forced by the one-scalar-operand limit of VOP3 on gfx950)
+template <class T>
+__device__ __forceinline__ T in_vgpr(T x) {
+  T y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
+  return y;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+
+template <int TRC, int TM, bool DESAT>
+__global__ __launch_bounds__(256) void k_tile(const FastParams F) {
+  __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
+  __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
+  __shared__ float2 cpair[2][CBH * CBW];       // per chroma sample: (top pair sum, bottom pair sum)
+  __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG : 1];
+  extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
+
+  const int t = threadIdx.x;
+  {
+    const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
+    for (int i = t; i < F.eq_n; i += 256)
+      eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
+    if (TRC == 0 && t < PQ_NSEG) {
+      const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
+      pq_lds[t] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
+    }
+  }
+
+  const unsigned lb = (unsigned)fxcd_remap(blockIdx.x, gridDim.x);
+  const unsigned bx = lb % F.nbx, bt = lb / F.nbx;
+  const unsigned by = bt % F.nby;
+  const int f = (int)(bt / F.nby);
+  const int px0 = (int)bx * TBW, py0 = (int)by * TBH, cx0 = (int)bx * CBW, cy0 = (int)by * CBH;
+  const int H = F.H, cw = F.cw, ch = F.ch;
+  // frame planes as buffer resources (block-uniform bases in SGPRs, 32-bit lane offsets)
+  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + f * F.in_fp[0], (long long)H * F.in_ls[0]);
+  const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + f * F.in_fp[1], (long long)ch * F.in_ls[1]);
+  const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + f * F.in_fp[2], (long long)ch * F.in_ls[2]);
+  const int lsy = (int)F.in_ls[0], lsc1 = (int)F.in_ls[1], lsc2 = (int)F.in_ls[2];
+
+  // ---- stage: luma tile, pre-scaled by ys (zimg depth conversion scale) ----
+  {
+    const int r = t >> 3, c = t & 7;
+    const int gy = py0 + r < H ? py0 + r : H - 1;
+    float v[8];
+    unpack8(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iy, gy * lsy + 2 * (px0 + 8 * c), 0, NT)), v);
+    float* d = yin + r * YST + 8 * c;
+    const float ys = F.ys;
+    *reinterpret_cast<float4*>(d) = make_float4(v[0] * ys, v[1] * ys, v[2] * ys, v[3] * ys);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ys, v[5] * ys, v[6] * ys, v[7] * ys);
+  }
+  // ---- stage: chroma rows cy0-1 .. cy0+16, horizontal pass (left siting,
+  // x2 scale): h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float ----
+  auto stage_chroma = [&](const __amdgpu_buffer_rsrc_t ic, int ls, float* plane, int rem) {
+    const int lr = rem >> 2, c = rem & 3;
+    const int off = fedge(cy0 - 1 + lr, ch) * ls;
+    float v[9];
+    unpack8(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, off + 2 * (cx0 + 8 * c), 0, NT)), v);
+    v[8] = (float)__builtin_amdgcn_raw_buffer_load_b16(ic, off + 2 * fedge(cx0 + 8 * c + 8, cw), 0, 0);
+    float* d = plane + lr * HST + 16 * c;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      *reinterpret_cast<float4*>(d + 4 * k) =
+          make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
+  };
+  // one thread stages the same chunk of both planes, so each buffer resource
+  // stays wave-uniform (a per-lane choice of resource becomes a waterfall loop)
+  if (t < 72) {
+    stage_chroma(iu, lsc1, hrow[0], t);
+    stage_chroma(iv, lsc2, hrow[1], t);
+  }
+  __syncthreads();
+
+  // ---- 8 steps; wave w, step s -> 8x8 sub-block (2w + (s&1), s>>1); lane =
+  // pixel (quad q = lane>>2 in a 4x4 quad grid, position lane&3 in the quad) ----
+  const int lane = t & 63, w = t >> 6;
+  const int qx = (lane >> 2) & 3, qy = lane >> 4, pxl = lane & 1, pyl = (lane >> 1) & 1;
+  const int xl = 16 * w + 2 * qx + pxl, yl = 2 * qy + pyl;                 // step (0,0) pixel
+  const float* ybase = yin + yl * YST + xl;
+  // vertical pass (centre siting): 3 x row cy + row cy-1 (top) / cy+1 (bottom)
+  const float* h0 = hrow[0] + (qy + 1) * HST + xl;
+  const float* h1 = hrow[1] + (qy + 1) * HST + xl;
+  const int hb = pyl ? HST : -HST;
+  float* cpb = reinterpret_cast<float*>(cpair[0]) + 2 * (qy * CBW + 8 * w + qx) + pyl;
+  // hot constants live in VGPRs
+  const float k_r = in_vgpr(F.k_r), k_g = in_vgpr(F.k_g), k_b = in_vgpr(F.k_b);
+  const float a_rv = in_vgpr(F.a_rv[1]), a_gv = in_vgpr(F.a_gv[1]), a_gu = in_vgpr(F.a_gu[1]), a_bu = in_vgpr(F.a_bu[1]);
+  const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
+  const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
+  const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
+  const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
+    const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
+    const int oc = 2 * (4 * (s >> 1) * CBW + 4 * (s & 1));
+    const float ybs = ybase[oy];
+    const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
+    const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
+    const float er = fmaf(V, a_rv, ybs + k_r);
+    const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + k_g));
+    const float eb = fmaf(U, a_bu, ybs + k_b);
+    float r, g, bl;
+    to_linear<TRC>(F, pq_lds, er, eg, eb, r, g, bl);
+    tone<TM, DESAT>(F, r, g, bl);
+    // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
+    // s < N-1 and the lattice cell index never needs a clamp
+    const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+    const float sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(g, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+    const float sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+    const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
+    const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
+    const bool rg = dr > dg, gb = dg > db, rb = dr > db;
+    const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
+    const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
+    const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
+    const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
+    const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
+#ifdef H2S_ABLATE_GATHER  // experiment only: every lane fetches lane 0's records
+    const int gb0 = __builtin_amdgcn_readfirstlane(base), gom = __builtin_amdgcn_readfirstlane(om),
+              goc = __builtin_amdgcn_readfirstlane(ocn);
+#else
+    const int gb0 = base, gom = om, goc = ocn;
+#endif
+    const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0, 0, 0);
+    const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0 + gom, 0, 0);
+    const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0 + goc, 0, 0);
+    const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0, F.c111, 0);
+    const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
+    const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+    // luma code (eq applied, shifted) replaces the luma sample this lane read
+    reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
+    // chroma: horizontal pair sums; both lanes of a pair store the same value
+    const float su = pair_sum(o.y), sv = pair_sum(o.z);
+    cpb[oc] = su;
+    cpb[oc + 2 * CBH * CBW] = sv;
+  }
+  __syncthreads();
+
+  // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
+  const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + f * F.out_fp[0], (long long)H * F.out_ls[0]);
+  {
+    const int r = t >> 3, c = t & 7;
+    if (py0 + r < H) {
+      const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
+      const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
+      const int off = (py0 + r) * (int)F.out_ls[0];
+      if (F.out8)
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
+            oy_, off + px0 + 8 * c, 0, NT);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
+            oy_, off + 2 * (px0 + 8 * c), 0, NT);
+    }
+  }
+  if (t < 128) {
+    // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
+    const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
+    if (cy0 + r < ch) {
+      const float4* src = reinterpret_cast<const float4*>(cpair[pl] + r * CBW + 8 * c);
+      unsigned code[8];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const float4 v = src[k];
+        code[2 * k] = (unsigned)(int)((v.x + v.y) + F.c_bias) << F.shift_out;
+        code[2 * k + 1] = (unsigned)(int)((v.z + v.w) + F.c_bias) << F.shift_out;
+      }
+      const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + f * F.out_fp[1 + pl], (long long)ch * F.out_ls[1 + pl]);
+      const int off = (cy0 + r) * (int)F.out_ls[1 + pl];
+      if (F.out8)
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
+                                               code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
+            oc_, off + cx0 + 8 * c, 0, NT);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
+                                               code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
+            oc_, off + 2 * (cx0 + 8 * c), 0, NT);
+    }
+  }
+}
+
+// YUV-premultiplied lattice (12-byte records, .cube order):
+// ((16 + 219*Y)*s + 0.5, 224*s*Cb/4, 224*s*Cr/4) with Y, Cb, Cr the BT.709
+// values of the clamped RGB lattice point, in the oracle's S6 operation order.
+__global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const YuvLutConsts K) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n3) return;
+  const float4 c = rgb[i];
+  const float R = clamp01(c.x), G = clamp01(c.y), B = clamp01(c.z);
+  const float Y = K.k709[0] * R + K.k709[1] * G + K.k709[2] * B;
+  const float cb = K.kcb[0] * R + K.kcb[1] * G + K.kcb[2] * B;
+  const float cr = K.kcr[0] * R + K.kcr[1] * G + K.kcr[2] * B;
+  const float s = K.s;
+  yuv[3 * i] = (16.0f + 219.0f * Y) * s + 0.5f;
+  yuv[3 * i + 1] = 224.0f * s * 0.25f * cb;
+  yuv[3 * i + 2] = 224.0f * s * 0.25f * cr;
+}
+
+#define FAST_CASES(X) \
+  X(0, 4, false)      \
+  X(0, 4, true)       \
+  X(0, 5, false)      \
+  X(0, 5, true)       \
+  X(0, 6, false)      \
+  X(0, 6, true)       \
+  X(0, 7, false)      \
+  X(1, 4, false)      \
+  X(1, 4, true)       \
+  X(1, 5, false)      \
+  X(1, 5, true)       \
+  X(1, 6, false)      \
+  X(1, 6, true)       \
+  X(1, 7, false)
+
+bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 7; }
+
+hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStream_t s) {
+  const long long nb = (long long)F.nbx * F.nby * F.nframes;
+  if (nb == 0) return hipSuccess;
+  dim3 grid((unsigned)nb), block(256);
+  const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
+  if (tm == 7) desat = false;
+#define X(T, M, D)                                                   \
+  if (trc == T && tm == M && desat == D) {                           \
+    hipLaunchKernelGGL((k_tile<T, M, D>), grid, block, lds, s, F);   \
+    return hipGetLastError();                                        \
+  }
+  FAST_CASES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st) {
+  const int n3 = n * n * n;
+  hipLaunchKernelGGL(k_build_lut_yuv, dim3((n3 + 255) / 256), dim3(256), 0, st, rgb, yuv, n3, K);
+  return hipGetLastError();
+}
+
+}  // namespace h2s

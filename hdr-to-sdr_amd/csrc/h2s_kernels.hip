@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
   const long long t = item / P.ngx;
   const int cy = (int)(t % P.ch);
   const int f = (int)(t / P.ch);
-  const int cx0 = gx * QPT;
+  const int cx0 = (gx + P.gx0) * QPT;
   const int cw = P.cw, ch = P.ch;
 
   // ---- chroma: rows cy-1, cy, cy+1; columns cx0 .. cx0+QPT (halo) ----

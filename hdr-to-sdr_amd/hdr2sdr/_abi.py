@@ -11,7 +11,7 @@ import math
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libh2s.so')
+LIB_PATH = os.environ.get('H2S_LIB') or os.path.join(_HERE, 'libh2s.so')
 
 # ---- error codes (include/h2s.h) ------------------------------------------
 H2S_OK = 0

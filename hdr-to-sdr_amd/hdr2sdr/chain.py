@@ -221,8 +221,19 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
                 raise ValueError(f'lut3d interp={interp} is not supported (reference uses tetrahedral)')
             lut_path = kv.get('file', pos[0] if pos else None)
             kw['lut_enabled'] = True
-        elif name == 'setparams':
-            continue  # metadata-only retag (src/utils.py:21-29)
+        elif name == 'libplacebo':
+            # GPU chain build_libplacebo_filter (src/utils.py:392-471): the
+            # tone map runs here natively.  libplacebo's own gamut/desat
+            # handling and peak_detect=1 (dynamic, temporally smoothed peak)
+            # are replaced by the static-peak operator: documented deviation.
+            tm = kv.get('tonemapping')
+            if tm is None:
+                raise ValueError('libplacebo stage without tonemapping=')
+            seen_linear = True
+            kw['tonemapper'] = tm.lower()
+            kw['desat'] = 0.0
+        elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
+            continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)
         elif name == 'eq':
             if set(kv) - {'gamma'}:
                 raise ValueError(f'eq options other than gamma are not supported: {kv}')

@@ -134,6 +134,9 @@ static float pq_encode_f(float y) {
 static float bt2390_sig(const ocfg *c, float sig) {
   float e1 = pq_encode_f(sig * (float)(c->p->npl / 10000.0));
   float e1n = (e1 - (float)c->src_min) / (float)(c->src_max - c->src_min);
+  /* E1 is clipped to the source range [Lb, Lw] (BT.2390-8 5.4); a NaN from an
+   * overflowed (inf) input counts as above the range */
+  e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);
   float ks = (float)c->ks, ml = (float)c->max_lum;
   float e2 = e1n;
   if (ks < 1.0f && e1n > ks) {

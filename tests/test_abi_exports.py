@@ -1,0 +1,95 @@
+"""The C-ABI library loads, exports every function include/h2s.h declares,
+and the ctypes mirrors of its structs have the C layout.  No compute calls:
+runs on the GPU-less build container."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import oracle
+from hdr2sdr import _abi
+
+from conftest import REPO, gpu_available
+
+HEADER = os.path.join(REPO, 'include', 'h2s.h')
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    names = re.findall(r'^\s*[A-Za-z_][\w\s\*]*?\b(h2s_\w+)\s*\(', src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_what_python_binds():
+    assert declared_functions() == sorted(_abi.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    L = ctypes.CDLL(_abi.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    out = subprocess.run(['nm', '-D', '--defined-only', _abi.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    for name in declared_functions():
+        assert re.search(rf'\bT {name}\b', out), f'{name} not exported as a text symbol'
+
+
+def test_abi_version_and_defaults():
+    L = _abi.lib()
+    assert L.h2s_abi_version() == 1
+    p = _abi.default_params()
+    assert (p.transfer_in, p.bits_in, p.bits_out, p.tonemap, p.desat, p.npl, p.gamma, p.lut_enabled) == \
+        (0, 10, 10, 6, 2.0, 100.0, 1.0, 1)
+    assert p.tm_param != p.tm_param  # NaN = filter default
+
+
+PROBE = r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "h2s.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(h2s_params), offsetof(h2s_params, tm_param),
+         offsetof(h2s_params, lut_enabled), offsetof(h2s_params, desat_luma), sizeof(h2s_frames),
+         offsetof(h2s_frames, width));
+  return 0;
+}
+'''
+
+
+def test_struct_layout_matches_c(tmp_path):
+    c = tmp_path / 'probe.c'
+    c.write_text(PROBE)
+    exe = tmp_path / 'probe'
+    subprocess.run(['gcc', '-I', os.path.dirname(HEADER), str(c), '-o', str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    for P, F in ((_abi.H2SParams, _abi.H2SFrames), (oracle.Params, oracle.Frames)):
+        want = [ctypes.sizeof(P), P.tm_param.offset, P.lut_enabled.offset, P.desat_luma.offset,
+                ctypes.sizeof(F), F.width.offset]
+        assert got == want
+
+
+@pytest.mark.skipif(gpu_available(), reason='checks the no-device error path')
+def test_create_without_device_fails_cleanly():
+    L = _abi.lib()
+    ctx = ctypes.c_void_p()
+    rc = L.h2s_create(0, ctypes.byref(ctx))
+    assert rc == _abi.H2S_E_HIP and not ctx.value
+    assert L.h2s_last_error(None)
+
+
+def test_null_handling_without_device():
+    L = _abi.lib()
+    assert L.h2s_set_lut(None, None, 65) == _abi.H2S_E_INVALID_ARG
+    assert L.h2s_set_params(None, None) == _abi.H2S_E_INVALID_ARG
+    assert L.h2s_process(None, None, None, 1, None) == _abi.H2S_E_INVALID_ARG
+    L.h2s_destroy(None)
+    assert L.h2s_cube_format(1, None, 0) == _abi.H2S_E_INVALID_ARG
+    with pytest.raises(ValueError):
+        _abi.raise_for(_abi.H2S_E_UNSUPPORTED, 'x')
+    with pytest.raises(FileNotFoundError):
+        _abi.raise_for(_abi.H2S_E_LUT_MISSING, 'x')
+    with pytest.raises(RuntimeError):
+        _abi.raise_for(_abi.H2S_E_HIP, 'x')

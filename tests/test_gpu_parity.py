@@ -51,18 +51,32 @@ def run_both(tm, params, kind, W, H, nframes=2, lut_n=65, seed=11):
     got = dst.to_numpy().buf.astype(np.int64)
     want = oracle.process(oracle.params_from(params.to_c()), lattice(lut_n) if params.lut_enabled else None,
                           src_cpu.to_numpy().buf, W, H).astype(np.int64)
-    return got, want, src_cpu
+    return got, want, (W, H)
 
 
-def assert_close_int(params, got, want, max_frac=5e-3):
+def assert_close_int(params, got, want, W, H, max_frac=5e-3):
+    """Chroma: |diff| <= one quantisation step.  Luma: eq runs after the
+    quantiser, so the bound is +-1 step *before* eq: got must lie between
+    eq[q-1] and eq[q+1] where eq[q] == want (eq is monotonic)."""
     q = params.bits_out if params.mode == 'native' else 8
-    step = 1 << (params.bits_out - q) if params.bits_out >= q else 1
-    diff = np.abs(got - want)
-    frac = float((diff > 0).mean())
-    assert diff.max() <= step, f'max diff {diff.max()} > step {step}'
+    shift = params.bits_out - q if params.bits_out >= q else 0
+    step = 1 << shift
+    ysz = W * H
+    gy, wy = got[:, :ysz] >> shift, want[:, :ysz] >> shift
+    gc, wc = got[:, ysz:], want[:, ysz:]
+    assert np.all(got % step == 0) and np.all(want % step == 0)
+    dc = np.abs(gc - wc)
+    assert dc.max(initial=0) <= step, f'chroma max diff {dc.max()} > step {step}'
+    eq = oracle.resolved(oracle.params_from(params.to_c()))[2].astype(np.int64)
+    lo_i = np.searchsorted(eq, wy, side='left')            # first q with eq[q] == want
+    hi_i = np.searchsorted(eq, wy, side='right') - 1       # last q with eq[q] == want
+    assert np.all(eq[np.clip(lo_i, 0, len(eq) - 1)] == wy), 'oracle luma not in eq table'
+    lo = eq[np.clip(lo_i - 1, 0, len(eq) - 1)]
+    hi = eq[np.clip(hi_i + 1, 0, len(eq) - 1)]
+    bad = (gy < lo) | (gy > hi)
+    assert not bad.any(), f'{int(bad.sum())} luma samples beyond +-1 pre-eq step'
+    frac = float(((np.abs(got - want)) > 0).mean())
     assert frac <= max_frac, f'{frac:.3%} of samples differ'
-    # differences, if any, are whole quantisation steps
-    assert np.all(diff % step == 0)
 
 
 CONFIGS = {
@@ -82,31 +96,31 @@ CONFIGS = {
 def test_configs_match_oracle(tm, cfg, kind):
     kw, lut_n = CONFIGS[cfg]
     params = hdr2sdr.TonemapParams(**kw)
-    got, want, _ = run_both(tm, params, kind, 128, 64, lut_n=lut_n)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, kind, 128, 64, lut_n=lut_n)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('mode', ['compat8', 'native'])
 @pytest.mark.parametrize('tmname', ['none', 'linear', 'gamma', 'clip', 'reinhard', 'hable', 'mobius', 'bt.2390'])
 def test_every_operator_both_modes(tm, tmname, mode):
     params = hdr2sdr.TonemapParams(tonemapper=tmname, gamma=1.3, bits_out=10, mode=mode)
-    got, want, _ = run_both(tm, params, 'smooth', 96, 48)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'smooth', 96, 48)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('desat_luma', ['rgb', 'bt2020', 'bt709'])
 @pytest.mark.parametrize('desat', [0.0, 2.0, 0.5])
 def test_desat_switches(tm, desat_luma, desat):
     params = hdr2sdr.TonemapParams(tonemapper='hable', desat=desat, desat_luma=desat_luma)
-    got, want, _ = run_both(tm, params, 'uniform', 64, 32)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'uniform', 64, 32)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('peak,maxcll,mastering', [(0, 0, 0), (0, 1000, 0), (0, 0, 4000), (0, 400, 1000), (5.0, 0, 0)])
 def test_peak_sources(tm, peak, maxcll, mastering):
     params = hdr2sdr.TonemapParams(tonemapper='reinhard', peak=peak, maxcll=maxcll, mastering_max=mastering)
-    got, want, _ = run_both(tm, params, 'ramp', 64, 32)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'ramp', 64, 32)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('W,H', [(2, 2), (4, 2), (6, 4), (18, 6), (130, 10), (1922, 4)])
@@ -114,21 +128,21 @@ def test_ragged_sizes_scalar_path(tm, W, H):
     """Widths that are not a multiple of the 8-pixel vector group, and
     1-row / 1-column chroma planes (edge rules on both sides)."""
     params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2)
-    got, want, _ = run_both(tm, params, 'uniform', W, H, nframes=3)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'uniform', W, H, nframes=3)
+    assert_close_int(params, got, want, *src_wh)
 
 
 def test_lut_disabled_closed_form(tm):
     params = hdr2sdr.TonemapParams(tonemapper='hable', lut_enabled=False)
-    got, want, _ = run_both(tm, params, 'ramp', 128, 64)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'ramp', 128, 64)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('lut_n', [2, 17, 33, 65])
 def test_lut_sizes(tm, lut_n):
     params = hdr2sdr.TonemapParams(tonemapper='mobius')
-    got, want, _ = run_both(tm, params, 'uniform', 64, 32, lut_n=lut_n)
-    assert_close_int(params, got, want)
+    got, want, src_wh = run_both(tm, params, 'uniform', 64, 32, lut_n=lut_n)
+    assert_close_int(params, got, want, *src_wh)
 
 
 @pytest.mark.parametrize('stage', [1, 2, 3, 4])
