@@ -1,0 +1,168 @@
+"""Oracle self-checks on CPU: known answers of each restated stage, the
+reference's parameter defaults, and frame-level properties.  The LUT stage
+itself is pinned against the reference generator in test_lut.py."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+import hdr2sdr
+from hdr2sdr.synth import synth_frames
+
+TM = {'none': 0, 'linear': 1, 'gamma': 2, 'clip': 3, 'reinhard': 4, 'hable': 5, 'mobius': 6, 'bt.2390': 7}
+
+
+def params(**kw):
+    if 'tonemap' in kw and isinstance(kw['tonemap'], str):
+        kw['tonemap'] = TM[kw['tonemap']]
+    return oracle.default_params(**kw)
+
+
+# ---- S1: ST 2084 / ARIB B67 (zimg) ---------------------------------------
+@pytest.mark.parametrize('code,nits', [(0.0, 0.0), (1.0, 10000.0), (0.5080784, 100.0), (0.7518271, 1000.0),
+                                       (0.9025723, 4000.0)])
+def test_pq_eotf_known_points(code, nits):
+    assert oracle.pq_eotf(code) * 10000.0 == pytest.approx(nits, rel=2e-5, abs=1e-6)
+
+
+def test_pq_eotf_clamps_negative_and_subthreshold():
+    assert oracle.pq_eotf(-0.3) == 0.0
+    assert oracle.pq_eotf(1e-8) == 0.0          # E^(1/m2) < c1 -> 0
+
+
+def test_hlg_inverse_oetf_known_points():
+    assert oracle.hlg_inverse_oetf(0.5) == pytest.approx(1.0 / 12.0, rel=1e-6)
+    assert oracle.hlg_inverse_oetf(0.25) == pytest.approx(0.25 ** 2 / 3.0, rel=1e-6)
+    assert oracle.hlg_inverse_oetf(1.0) == pytest.approx(1.0, rel=1e-5)
+    assert oracle.hlg_inverse_oetf(-1.0) == 0.0
+
+
+# ---- S2: vf_tonemap curves and init defaults -------------------------------
+def test_tonemap_param_defaults_match_vf_tonemap():
+    assert oracle.resolved(params(tonemap='reinhard'))[1] == 1.0          # NaN -> 1.0
+    assert oracle.resolved(params(tonemap='reinhard', tm_param=0.5))[1] == 1.0   # (1-p)/p
+    assert oracle.resolved(params(tonemap='reinhard', tm_param=0.25))[1] == 3.0
+    assert oracle.resolved(params(tonemap='mobius'))[1] == pytest.approx(0.3)
+    assert oracle.resolved(params(tonemap='gamma'))[1] == pytest.approx(1.8)
+    assert oracle.resolved(params(tonemap='hable'))[1] == 1.0
+
+
+@pytest.mark.parametrize('kw,peak', [({}, 10.0), ({'maxcll': 1000.0}, 10.0), ({'mastering_max': 4000.0}, 40.0),
+                                     ({'maxcll': 400.0, 'mastering_max': 1000.0}, 4.0), ({'peak': 5.0}, 5.0)])
+def test_signal_peak_resolution(kw, peak):
+    """ff_determine_signal_peak: MaxCLL, then mastering max, then the
+    linear-trc default 10 (REFERENCE_WHITE 100)."""
+    assert oracle.resolved(params(**kw))[0] == pytest.approx(peak)
+
+
+def test_tone_curve_known_answers():
+    assert oracle.tone_curve(params(tonemap='hable'), 10.0) == pytest.approx(1.0, rel=1e-6)      # sig = peak
+    assert oracle.tone_curve(params(tonemap='reinhard'), 10.0) == pytest.approx(1.0, rel=1e-6)
+    assert oracle.tone_curve(params(tonemap='mobius'), 0.2) == pytest.approx(0.2, rel=1e-7)      # identity <= j
+    assert oracle.tone_curve(params(tonemap='mobius'), 10.0) == pytest.approx(1.0, rel=1e-5)
+    assert oracle.tone_curve(params(tonemap='linear'), 2.0) == pytest.approx(0.2, rel=1e-6)      # sig * 1/peak
+    assert oracle.tone_curve(params(tonemap='clip'), 3.0) == pytest.approx(1.0)
+    assert oracle.tone_curve(params(tonemap='none'), 3.0) == pytest.approx(3.0)
+    # hable(0)-based curve passes through ~0 and is monotonic
+    xs = np.linspace(1e-4, 20, 200)
+    ys = [oracle.tone_curve(params(tonemap='hable'), float(x)) for x in xs]
+    assert ys[0] < 1e-3 and all(b >= a for a, b in zip(ys, ys[1:]))
+
+
+def test_bt2390_eetf_shape():
+    p = params(tonemap='bt.2390')
+    assert oracle.tone_curve(p, 0.01) == pytest.approx(0.01, rel=1e-3)     # below the knee: identity
+    top = oracle.tone_curve(p, 10.0)                                        # source peak -> target peak
+    assert top == pytest.approx(1.0, rel=1e-3)
+    assert oracle.tone_curve(p, 100.0) == pytest.approx(top, rel=1e-6)      # clipped to source range
+
+
+# ---- S7: vf_eq create_lut ---------------------------------------------------
+def eq_reference(gamma, bits):
+    n = 1 << bits
+    out = []
+    for i in range(n):
+        v = i / (n - 1)
+        if v <= 0.0:
+            out.append(0)
+            continue
+        v = math.pow(v, 1.0 / gamma)
+        out.append(n - 1 if v >= 1.0 else int(n * v))
+    return np.array(out)
+
+
+@pytest.mark.parametrize('gamma', [1.0, 2.2, 0.5, 1.3, 3.0, 0.1])
+@pytest.mark.parametrize('mode,bits_out', [(0, 10), (1, 10), (1, 12), (0, 8)])
+def test_eq_lut(gamma, mode, bits_out):
+    q = bits_out if mode == 1 else 8
+    eq = oracle.resolved(params(gamma=gamma, mode=mode, bits_out=bits_out))[2]
+    assert np.array_equal(eq, eq_reference(gamma, q))
+    if gamma == 1.0:
+        assert np.array_equal(eq, np.arange(1 << q))
+
+
+# ---- frame level ----------------------------------------------------------
+LAT = None
+
+
+def lattice():
+    global LAT
+    if LAT is None:
+        LAT = hdr2sdr.generate_lattice(65)
+    return LAT
+
+
+def grey_frames(bits=10, w=64, h=8):
+    fb = hdr2sdr.FrameBatch.empty_numpy(1, w, h, bits)
+    s = 1 << (bits - 8)
+    fb.y[0] = np.linspace(16 * s, 235 * s, w).astype(np.uint16)[None, :]
+    fb.u[0] = 128 * s
+    fb.v[0] = 128 * s
+    return fb
+
+
+@pytest.mark.parametrize('tm', ['reinhard', 'hable', 'mobius', 'bt.2390'])
+@pytest.mark.parametrize('bits', [10, 12])
+def test_neutral_axis_stays_neutral_and_monotonic(tm, bits):
+    fb = grey_frames(bits)
+    p = params(tonemap=tm, bits_in=bits, bits_out=bits, transfer_in=0 if bits == 10 else 1)
+    out = hdr2sdr.FrameBatch(oracle.process(p, lattice(), fb.buf, fb.width, fb.height), fb.width, fb.height, bits)
+    mid = 128 << (bits - 8)
+    assert np.abs(out.u.astype(int) - mid).max() <= 1 << (bits - 8)
+    assert np.abs(out.v.astype(int) - mid).max() <= 1 << (bits - 8)
+    row = out.y[0, 0].astype(int)
+    assert np.all(np.diff(row) >= 0) and row[0] == 16 << (bits - 8)
+
+
+def test_compat8_output_is_8bit_shifted_and_native_is_not():
+    fb = synth_frames('smooth', 1, 64, 32, 10, seed=4).to_numpy()
+    c8 = oracle.process(params(tonemap='hable', mode=0), lattice(), fb.buf, 64, 32)
+    nat = oracle.process(params(tonemap='hable', mode=1), lattice(), fb.buf, 64, 32)
+    assert np.all(c8 % 4 == 0)
+    assert np.any(nat % 4 != 0)
+    assert np.abs(c8.astype(int) - nat.astype(int)).max() <= 4
+
+
+def test_lut_chain_tracks_closed_form_gamut_math():
+    """Analog of the reference smoke test TestLutReproducesLegacyGamutMath
+    (test/smoke_test.py:264-343): the 65^3 tetrahedral LUT chain and the
+    closed-form zscale p=bt709 chain (FFMPEG_FILTER_LEGACY_NO_LUT) agree within
+    12/255 on a 21x21 sample grid (reference tolerance :300)."""
+    W, H = 960, 540
+    fb = synth_frames('smooth', 1, W, H, 10, seed=21).to_numpy()
+    lut_rgb = oracle.debug_float(params(tonemap='reinhard'), lattice(), fb.buf, W, H, 4)
+    legacy = oracle.debug_float(params(tonemap='reinhard', lut_enabled=0), None, fb.buf, W, H, 4)
+    ys = np.arange(0, H, max(1, H // 20))
+    xs = np.arange(0, W, max(1, W // 20))
+    a = np.round(np.clip(lut_rgb[:, ys][:, :, xs], 0, 1) * 255)
+    b = np.round(np.clip(legacy[:, ys][:, :, xs], 0, 1) * 255)
+    assert np.abs(a - b).max() <= 12
+
+
+def test_multithreaded_oracle_is_deterministic():
+    fb = synth_frames('uniform', 3, 128, 64, 10, seed=2).to_numpy()
+    p = params(tonemap='hable', gamma=2.2)
+    a = oracle.process(p, lattice(), fb.buf, 128, 64, nthreads=1)
+    b = oracle.process(p, lattice(), fb.buf, 128, 64, nthreads=4)
+    assert np.array_equal(a, b)
