@@ -68,12 +68,28 @@ def cpu_baseline(params, lattice, width, height, budget_s):
         oracle.process(p, lattice, buf, width, height, nthreads=cores)
         n += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or n >= 64:
+        if el >= budget_s or n >= 1024:
             break
     mpx = n * width * height / el / 1e6
     return {'value': round(mpx, 3), 'unit': 'Mpixel/s', 'cores': cores, 'kind': 'port',
             'sample': f'{n} x {width}x{height} smooth frame(s), same chain/params, {el:.1f} s, '
                       f'oracle/h2s_oracle.c (C restatement of the ffmpeg chain, not ffmpeg) with {cores} OpenMP threads'}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per k_tile dispatch from the committed PMC passes
+    (scripts/profile.sh -> prof_summary.py -> profiles/<round>/traffic.json),
+    used only when they were measured on this exact workload."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', '*', 'traffic.json')), reverse=True):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if rec.get('workload') == workload:
+            rec['source'] = os.path.relpath(f, REPO) + ' (' + rec.get('method', '') + ')'
+            return rec
+    return None
 
 
 def main():
@@ -82,6 +98,7 @@ def main():
     import torch.distributed as dist
 
     import hdr2sdr
+    from hdr2sdr.dist import broadcast_setup, frame_checksum, reduce_run, shard_range
     from hdr2sdr.synth import synth_frames
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -95,21 +112,21 @@ def main():
 
     params = hdr2sdr.TonemapParams(tonemapper=args.tonemapper, gamma=args.gamma, bits_in=args.bits_in,
                                    bits_out=args.bits_out, transfer=args.transfer, mode=args.mode)
-    # LUT lattice: generated on rank 0, broadcast over RCCL (frames never move)
+    # params + LUT lattice: built on rank 0, broadcast over RCCL (frames never move)
     n = args.lut
-    lat = torch.empty((n ** 3, 3), dtype=torch.float32, device=dev)
-    if rank == 0:
-        lat.copy_(torch.from_numpy(hdr2sdr.generate_lattice(n)))
+    lattice_host = hdr2sdr.generate_lattice(n) if rank == 0 else None
     if world > 1:
-        dist.broadcast(lat, src=0)
-    lattice_host = lat.cpu().numpy()
+        params, lattice_host = broadcast_setup(params if rank == 0 else None, lattice_host, n, dev)
 
     tm = hdr2sdr.Tonemapper(local, params, lattice_host)
     W, H, B = args.width, args.height, args.frames
 
     def run(kind):
-        src = synth_frames(kind, B, W, H, args.bits_in, device=dev, seed=0x5EED + rank * B)
-        dst = hdr2sdr.FrameBatch.empty_torch(B, W, H, args.bits_out, dev)
+        # this rank's frames: global indices [rank*B, rank*B + B) of a
+        # world*B-frame sequence (shard_range), synthesised in place
+        a, b = shard_range(world * B, world, rank)
+        src = synth_frames(kind, b - a, W, H, args.bits_in, device=dev, seed=0x5EED + a)
+        dst = hdr2sdr.FrameBatch.empty_torch(b - a, W, H, args.bits_out, dev)
         stream = torch.cuda.current_stream(dev)
         for _ in range(args.warmup):
             tm.process(src, dst, stream)
@@ -125,20 +142,20 @@ def main():
         el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
         kms = tm.kernel_ms(args.steps)
         tm.set_timing(False)
+        px = (b - a) * W * H * args.steps
+        cks = frame_checksum(dst.buf, a)
+        if world > 1:
+            px, cks, el = reduce_run(px, cks, el, dev)
         del src, dst
-        return el, kms
+        return el, kms, px, cks
 
-    el, kms = run(args.kind)
+    el, kms, px_total, checksum = run(args.kind)
     alt = None
     if not args.no_alt:
-        el_u, kms_u = run('uniform')
-        alt = {'kind': 'uniform', 'value': round(world * args.steps * B * W * H / el_u / 1e6, 1),
-               'kernel_ms': round(kms_u, 4)}
+        el_u, kms_u, px_u, _ = run('uniform')
+        alt = {'kind': 'uniform', 'value': round(px_u / el_u / 1e6, 1), 'kernel_ms': round(kms_u, 4)}
 
     if rank != 0:
         if world > 1:
@@ -148,9 +165,9 @@ def main():
     sb_in = 1 if args.bits_in == 8 else 2
     sb_out = 1 if args.bits_out == 8 else 2
     bytes_per_px = 1.5 * sb_in + 1.5 * sb_out
-    value = world * args.steps * px_per_launch / el / 1e6
+    value = px_total / el / 1e6
     achieved = bytes_per_px * px_per_launch / (kms / 1e3) / 1e9
-    lut_bytes = n ** 3 * 16
+    lut_bytes = n ** 3 * 12     # YUV-premultiplied lattice records read by k_tile
     rec = {
         'metric': 'Mpixel/s HDR10->SDR (4K frames) at 1/2/4/8 GPUs; % HBM roofline',
         'value': round(value, 1),
@@ -180,7 +197,7 @@ def main():
             'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
             'traffic': None,
-            'kernel': 'k_process (h2s_kernels.hip)',
+            'kernel': 'k_tile (h2s_fast.hip)',
             'kernel_ms': round(kms, 4),
             'bytes_per_px': bytes_per_px,
             'algorithmic_bytes_per_launch': int(bytes_per_px * px_per_launch),
@@ -188,6 +205,11 @@ def main():
         },
         'cpu_baseline': None,
     }
+    tr = pmc_traffic(rec['config']['workload'])
+    if tr is not None:
+        rec['roofline']['traffic'] = tr['bytes_per_dispatch']
+        rec['roofline']['traffic_source'] = tr['source']
+    rec['config']['output_checksum'] = checksum
     if world == 1 and args.cpu_seconds > 0:
         rec['cpu_baseline'] = cpu_baseline(params, lattice_host, W, H, args.cpu_seconds)
     print(json.dumps(rec), flush=True)

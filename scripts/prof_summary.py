@@ -1,8 +1,11 @@
 """Summarise a scripts/profile.sh directory: per-kernel average duration from
 the kernel-trace stats and per-dispatch averages of every PMC counter for
-k_process, with the gfx950 FETCH_SIZE correction (x2 for wide coalesced
-streaming reads, MI355X_MICROARCH.md §HBM)."""
+k_tile, with the gfx950 FETCH_SIZE correction (x2 for wide coalesced
+streaming reads, MI355X_MICROARCH.md §HBM).  Also writes traffic.json (HBM
+bytes per dispatch + the bench workload it was measured on), which bench.py
+reports as roofline.traffic when its own workload matches."""
 import csv
+import json
 import glob
 import os
 import sys
@@ -24,7 +27,7 @@ for f in glob.glob(os.path.join(d, 'pmc_*', '**', '*counter_collection.csv'), re
         if KERNEL not in row.get('Kernel_Name', ''):
             continue
         vals[row['Counter_Name']].append(float(row['Counter_Value']))
-print('## PMC per k_process dispatch (mean over dispatches)')
+print('## PMC per k_tile dispatch (mean over dispatches)')
 for k in sorted(vals):
     v = vals[k]
     print(f'{k:28s} {sum(v) / len(v):18.1f}   (n={len(v)})')
@@ -34,3 +37,19 @@ if 'FETCH_SIZE' in vals:
 if 'WRITE_SIZE' in vals:
     ws = sum(vals['WRITE_SIZE']) / len(vals['WRITE_SIZE'])
     print(f'WRITE_SIZE (KiB->B): {ws * 1024:.0f} B per dispatch')
+
+if 'FETCH_SIZE' in vals and 'WRITE_SIZE' in vals:
+    workload = None
+    log = os.path.join(d, 'pmc_fetch.log')
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith('{'):
+                workload = json.loads(line)['config']['workload']
+    rec = {'kernel': KERNEL, 'workload': workload,
+           'fetch_bytes_per_dispatch': int(fs * 2 * 1024), 'write_bytes_per_dispatch': int(ws * 1024),
+           'bytes_per_dispatch': int(fs * 2 * 1024 + ws * 1024),
+           'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950), KiB->B',
+           'dispatches': len(vals['FETCH_SIZE'])}
+    with open(os.path.join(d, 'traffic.json'), 'w') as f:
+        json.dump(rec, f, indent=1)
+    print('traffic.json:', json.dumps(rec))

@@ -1,0 +1,108 @@
+"""N>1 path on CPU: gloo, world_size 2.
+
+Each rank receives params + lattice from rank 0, converts only its frame
+shard, and the SUM/MAX reduction must reproduce the single-process result.
+The per-frame converter here is the oracle (test infrastructure): what is
+under test is the sharding and the collectives, which are identical on the
+RCCL/GPU path (bench.py)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from hdr2sdr.dist import frame_checksum, owner_of, shard_range
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize('nframes,world', [(512, 8), (5, 2), (1, 2), (0, 4), (7, 3), (64, 1)])
+def test_shard_range_partitions(nframes, world):
+    seen = []
+    for r in range(world):
+        a, b = shard_range(nframes, world, r)
+        assert 0 <= a <= b <= nframes
+        seen.extend(range(a, b))
+        for i in range(a, b):
+            assert owner_of(i, nframes, world) == r
+    assert seen == list(range(nframes))
+
+
+def test_c4_shards_64_per_rank():
+    assert [shard_range(512, 8, r) for r in range(8)] == [(64 * r, 64 * r + 64) for r in range(8)]
+
+
+def test_shard_range_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+NFRAMES, W, H = 5, 64, 32
+
+
+def _worker(rank, world, port, out_dir):
+    for p in (os.path.join(REPO, 'hdr-to-sdr_amd'), REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from hdr2sdr import TonemapParams, generate_lattice
+    from hdr2sdr.dist import broadcast_setup, frame_checksum, reduce_run, shard_range
+    from hdr2sdr.synth import synth_frames
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        params = TonemapParams(tonemapper='hable', gamma=2.2) if rank == 0 else None
+        lattice = generate_lattice(17) if rank == 0 else None
+        params, lattice = broadcast_setup(params, lattice, 17)
+        a, b = shard_range(NFRAMES, world, rank)
+        # each rank synthesises only its own frames (seed = base + global index)
+        src = synth_frames('smooth', b - a, W, H, 10, seed=0x5EED + a).to_numpy() if b > a else None
+        if src is not None:
+            out = oracle.process(oracle.params_from(params.to_c()), lattice, src.buf, W, H, nthreads=1)
+            cks = frame_checksum(out, a)
+        else:
+            cks = 0
+        px, total, el = reduce_run((b - a) * W * H, cks, 0.25 * (rank + 1))
+        np.save(os.path.join(out_dir, f'r{rank}.npy'),
+                np.array([px, total, el, float(lattice.sum()), params.gamma], dtype=np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_matches_single_process(tmp_path):
+    import oracle
+    from hdr2sdr import TonemapParams, generate_lattice
+    from hdr2sdr.synth import synth_frames
+
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method='spawn')
+    res = [np.load(tmp_path / f'r{r}.npy') for r in range(world)]
+
+    lat = generate_lattice(17)
+    p = oracle.params_from(TonemapParams(tonemapper='hable', gamma=2.2).to_c())
+    src = synth_frames('smooth', NFRAMES, W, H, 10, seed=0x5EED).to_numpy()
+    want = frame_checksum(oracle.process(p, lat, src.buf, W, H, nthreads=1), 0)
+    for r in res:
+        assert int(r[0]) == NFRAMES * W * H          # SUM of pixels
+        assert int(r[1]) == want                       # SUM of shard checksums == whole-sequence checksum
+        assert r[2] == pytest.approx(0.5)              # MAX of elapsed
+        assert r[3] == pytest.approx(float(lat.sum()))  # lattice broadcast
+        assert r[4] == 2.2                             # params broadcast
+
+
+def test_frame_checksum_is_order_sensitive():
+    a = np.arange(12, dtype=np.uint16).reshape(3, 4)
+    assert frame_checksum(a, 0) == frame_checksum(a[:2], 0) + frame_checksum(a[2:], 2)
+    assert frame_checksum(a[::-1].copy(), 0) != frame_checksum(a, 0)
