@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -38,6 +39,7 @@ struct h2s_ctx {
   float* d_lut_yuv = nullptr;  // lattice pre-multiplied into output code space (3 floats/point)
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
   bool fast_enabled = true;
+  int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   void* d_stage = nullptr;
@@ -388,6 +390,10 @@ int h2s_create(int device, h2s_ctx** out) {
   if (!c) return fail(nullptr, H2S_E_OOM, "context allocation failed");
   c->device = device;
   h2s_params_default(&c->params);
+  if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
+    const int tpb = atoi(v);
+    if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
+  }
   *out = c;
   return 0;
 }
@@ -623,6 +629,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     F.nbx = (unsigned)(k.W / 64);
     F.nby = (unsigned)((k.H + 31) / 32);
     F.nframes = (unsigned)nframes;
+    F.tpb = c->tiles_per_block;
     e = h2s::launch_fast(F, k.transfer, k.tonemap, k.desat_on != 0, s);
   } else {
     e = h2s::launch_process(k, vec, out8, s);

@@ -58,6 +58,7 @@ struct KParams {
 struct FastParams {
   int W, H, cw, ch;                // luma / chroma geometry (W % 64 == 0)
   unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
+  int tpb;                         // tiles walked by one block (k_tile prefetches tile i+1 during tile i)
   const uint8_t* in[3];
   long long in_ls[3], in_fp[3];
   uint8_t* out[3];

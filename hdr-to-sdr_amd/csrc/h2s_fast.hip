@@ -65,25 +65,30 @@ __device__ __forceinline__ float pq_exact(const FastParams& F, float e) {
   return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + F.log2_lin_scale);
 }
 
-// table form: 4 full-rate VALU + 2 half-rate + one LDS read, no transcendentals
+// table form: 4 full-rate VALU + 2 half-rate + one LDS read, no transcendentals.
+// ESC = PQ_SEG when the caller already scaled e by PQ_SEG (folded into the
+// Y'CbCr->R'G'B' constants), 1 otherwise.
+template <int ESC>
 __device__ __forceinline__ float pq_table(const float4* tab, float e) {
-  const float u = __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * 0.99999994f) * (float)PQ_SEG;
+  const float u = ESC == 1 ? __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * 0.99999994f) * (float)PQ_SEG
+                           : __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * (float)PQ_SEG * 0.99999994f);
   const float4 c = tab[(int)u];
   const float t = __builtin_amdgcn_fractf(u);
   return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
 }
 
 // S1 transfer to linear (units of npl), specialised
-template <int TRC>
+template <int TRC, int ESC = 1>
 __device__ __forceinline__ void to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
                                           float& r, float& g, float& b) {
   if (TRC == 0) {
-    r = pq_table(pq_lds, er), g = pq_table(pq_lds, eg), b = pq_table(pq_lds, eb);
+    r = pq_table<ESC>(pq_lds, er), g = pq_table<ESC>(pq_lds, eg), b = pq_table<ESC>(pq_lds, eb);
     const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
-    if (__builtin_amdgcn_ballot_w64(emax >= PQ_EMAX)) {  // rare: extreme out-of-gamut codes
-      r = er >= PQ_EMAX ? pq_exact(F, er) : r;
-      g = eg >= PQ_EMAX ? pq_exact(F, eg) : g;
-      b = eb >= PQ_EMAX ? pq_exact(F, eb) : b;
+    constexpr float EL = PQ_EMAX * (float)ESC, EI = 1.0f / (float)ESC;
+    if (__builtin_amdgcn_ballot_w64(emax >= EL)) {  // rare: extreme out-of-gamut codes
+      r = er >= EL ? pq_exact(F, er * EI) : r;
+      g = eg >= EL ? pq_exact(F, eg * EI) : g;
+      b = eb >= EL ? pq_exact(F, eb * EI) : b;
     }
   } else {
     // zimg arib_b67_inverse_oetf, branch-free; then the OOTF (gamma 1.2)
@@ -182,72 +187,93 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
 }
 
+// one tile's global loads, held in registers between issue and the LDS commit
+struct TileRegs {
+  uint4 ya, ua, va;
+  unsigned uh, vh;
+};
+
+struct TileGeo {
+  int f, px0, py0, cx0, cy0;
+};
+
+__device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) {
+  const unsigned bx = tile % F.nbx, bt = tile / F.nbx;
+  TileGeo g;
+  g.f = (int)(bt / F.nby);
+  const int by = (int)(bt % F.nby);
+  g.px0 = (int)bx * TBW, g.py0 = by * TBH, g.cx0 = (int)bx * CBW, g.cy0 = by * CBH;
+  return g;
+}
+
+// issue (do not wait for) the loads of one tile: luma 64 x 32 (one 16-byte
+// load per thread) and chroma rows cy0-1 .. cy0+16 (18 rows x 4 chunks of 8
+// samples + 1 right-halo sample; threads 0..71).  One thread loads the same
+// chunk of both planes, so each buffer resource stays wave-uniform (a per-lane
+// choice of resource becomes a waterfall loop).
+__device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t) {
+  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], (long long)F.H * F.in_ls[0]);
+  const int yr = t >> 3, yc = t & 7;
+  TileRegs r;
+  r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                       iy, (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), 0, NT));
+  r.ua = r.va = make_uint4(0, 0, 0, 0);
+  r.uh = r.vh = 0;
+  if (t < 72) {
+    const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], (long long)F.ch * F.in_ls[1]);
+    const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], (long long)F.ch * F.in_ls[2]);
+    const int clr = t >> 2, ccx = t & 3;
+    const int row = fedge(g.cy0 - 1 + clr, F.ch), hx = 2 * fedge(g.cx0 + 8 * ccx + 8, F.cw);
+    const int ou = row * (int)F.in_ls[1], ov = row * (int)F.in_ls[2];
+    r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iu, ou + 2 * (g.cx0 + 8 * ccx), 0, NT));
+    r.va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iv, ov + 2 * (g.cx0 + 8 * ccx), 0, NT));
+    r.uh = __builtin_amdgcn_raw_buffer_load_b16(iu, ou + hx, 0, 0);
+    r.vh = __builtin_amdgcn_raw_buffer_load_b16(iv, ov + hx, 0, 0);
+  }
+  return r;
+}
+
+// Each block walks F.tpb consecutive tiles (XCD-remapped, so neighbouring
+// tiles and their lattice cells share one XCD's L2).  The loads of tile i+1
+// are issued before tile i is computed, so after the first tile the block no
+// longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
+// barrier, 8 compute steps, barrier, store, barrier.
 template <int TRC, int TM, bool DESAT>
-__global__ __launch_bounds__(256) void k_tile(const FastParams F) {
+// 5 waves per SIMD is the LDS-bound occupancy (5 blocks x 31 KB per CU): let
+// the compiler use the VGPRs that allows (<= 96), no more
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float2 cpair[2][CBH * CBW];       // per chroma sample: (top pair sum, bottom pair sum)
   __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG : 1];
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
+  // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
+  // folded into the Y'CbCr->R'G'B' constants)
+  constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
 
   const int t = threadIdx.x;
-  {
-    const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
-    for (int i = t; i < F.eq_n; i += 256)
-      eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
-    if (TRC == 0 && t < PQ_NSEG) {
-      const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
-      pq_lds[t] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
-    }
-  }
+  const unsigned ntiles = F.nbx * F.nby * F.nframes;
+  unsigned tile = (unsigned)fxcd_remap(blockIdx.x, gridDim.x) * (unsigned)F.tpb;
+  const unsigned tend = tile + (unsigned)F.tpb < ntiles ? tile + (unsigned)F.tpb : ntiles;
 
-  const unsigned lb = (unsigned)fxcd_remap(blockIdx.x, gridDim.x);
-  const unsigned bx = lb % F.nbx, bt = lb / F.nbx;
-  const unsigned by = bt % F.nby;
-  const int f = (int)(bt / F.nby);
-  const int px0 = (int)bx * TBW, py0 = (int)by * TBH, cx0 = (int)bx * CBW, cy0 = (int)by * CBH;
-  const int H = F.H, cw = F.cw, ch = F.ch;
-  // frame planes as buffer resources (block-uniform bases in SGPRs, 32-bit lane offsets)
-  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + f * F.in_fp[0], (long long)H * F.in_ls[0]);
-  const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + f * F.in_fp[1], (long long)ch * F.in_ls[1]);
-  const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + f * F.in_fp[2], (long long)ch * F.in_ls[2]);
-  const int lsy = (int)F.in_ls[0], lsc1 = (int)F.in_ls[1], lsc2 = (int)F.in_ls[2];
-
-  // ---- stage: luma tile, pre-scaled by ys (zimg depth conversion scale) ----
-  {
-    const int r = t >> 3, c = t & 7;
-    const int gy = py0 + r < H ? py0 + r : H - 1;
-    float v[8];
-    unpack8(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iy, gy * lsy + 2 * (px0 + 8 * c), 0, NT)), v);
-    float* d = yin + r * YST + 8 * c;
-    const float ys = F.ys;
-    *reinterpret_cast<float4*>(d) = make_float4(v[0] * ys, v[1] * ys, v[2] * ys, v[3] * ys);
-    *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ys, v[5] * ys, v[6] * ys, v[7] * ys);
+  // ---- prologue: first tile + tables, all issued before any wait ----
+  TileGeo geo = tile_geo(F, tile);
+  TileRegs cur = tile_load(F, geo, t);
+  const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
+  const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * t, 0, 0);  // out of range -> 0
+  float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (TRC == 0 && t < PQ_NSEG) {
+    const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
+    pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
   }
-  // ---- stage: chroma rows cy0-1 .. cy0+16, horizontal pass (left siting,
-  // x2 scale): h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float ----
-  auto stage_chroma = [&](const __amdgpu_buffer_rsrc_t ic, int ls, float* plane, int rem) {
-    const int lr = rem >> 2, c = rem & 3;
-    const int off = fedge(cy0 - 1 + lr, ch) * ls;
-    float v[9];
-    unpack8(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, off + 2 * (cx0 + 8 * c), 0, NT)), v);
-    v[8] = (float)__builtin_amdgcn_raw_buffer_load_b16(ic, off + 2 * fedge(cx0 + 8 * c + 8, cw), 0, 0);
-    float* d = plane + lr * HST + 16 * c;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      *reinterpret_cast<float4*>(d + 4 * k) =
-          make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
-  };
-  // one thread stages the same chunk of both planes, so each buffer resource
-  // stays wave-uniform (a per-lane choice of resource becomes a waterfall loop)
-  if (t < 72) {
-    stage_chroma(iu, lsc1, hrow[0], t);
-    stage_chroma(iv, lsc2, hrow[1], t);
-  }
-  __syncthreads();
+  if (t < F.eq_n) eq_lds[t] = (uint16_t)(eq0 << F.shift_out);
+  for (int i = t + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
+    eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
+  if (TRC == 0 && t < PQ_NSEG) pq_lds[t] = pq0;
 
-  // ---- 8 steps; wave w, step s -> 8x8 sub-block (2w + (s&1), s>>1); lane =
-  // pixel (quad q = lane>>2 in a 4x4 quad grid, position lane&3 in the quad) ----
+  // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block
+  // (2w + (s&1), s>>1); lane = pixel (quad q = lane>>2 in a 4x4 quad grid,
+  // position lane&3 in the quad) ----
   const int lane = t & 63, w = t >> 6;
   const int qx = (lane >> 2) & 3, qy = lane >> 4, pxl = lane & 1, pyl = (lane >> 1) & 1;
   const int xl = 16 * w + 2 * qx + pxl, yl = 2 * qy + pyl;                 // step (0,0) pixel
@@ -257,104 +283,138 @@ __global__ __launch_bounds__(256) void k_tile(const FastParams F) {
   const float* h1 = hrow[1] + (qy + 1) * HST + xl;
   const int hb = pyl ? HST : -HST;
   float* cpb = reinterpret_cast<float*>(cpair[0]) + 2 * (qy * CBW + 8 * w + qx) + pyl;
-  // hot constants live in VGPRs
-  const float k_r = in_vgpr(F.k_r), k_g = in_vgpr(F.k_g), k_b = in_vgpr(F.k_b);
-  const float a_rv = in_vgpr(F.a_rv[1]), a_gv = in_vgpr(F.a_gv[1]), a_gu = in_vgpr(F.a_gu[1]), a_bu = in_vgpr(F.a_bu[1]);
-  const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
-  const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
-  const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
-  const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
-#pragma unroll
-  for (int s = 0; s < 8; s++) {
-    const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
-    const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
-    const int oc = 2 * (4 * (s >> 1) * CBW + 4 * (s & 1));
-    const float ybs = ybase[oy];
-    const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
-    const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
-    const float er = fmaf(V, a_rv, ybs + k_r);
-    const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + k_g));
-    const float eb = fmaf(U, a_bu, ybs + k_b);
-    float r, g, bl;
-    to_linear<TRC>(F, pq_lds, er, eg, eb, r, g, bl);
-    tone<TM, DESAT>(F, r, g, bl);
-    // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
-    // s < N-1 and the lattice cell index never needs a clamp
-    const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-    const float sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(g, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-    const float sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-    const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-    const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
-    const bool rg = dr > dg, gb = dg > db, rb = dr > db;
-    const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
-    const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
-    const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
-    const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
-    const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
-#ifdef H2S_ABLATE_GATHER  // experiment only: every lane fetches lane 0's records
-    const int gb0 = __builtin_amdgcn_readfirstlane(base), gom = __builtin_amdgcn_readfirstlane(om),
-              goc = __builtin_amdgcn_readfirstlane(ocn);
-#else
-    const int gb0 = base, gom = om, goc = ocn;
-#endif
-    const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0, 0, 0);
-    const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0 + gom, 0, 0);
-    const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0 + goc, 0, 0);
-    const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, gb0, F.c111, 0);
-    const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
-    const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
-    // luma code (eq applied, shifted) replaces the luma sample this lane read
-    reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
-    // chroma: horizontal pair sums; both lanes of a pair store the same value
-    const float su = pair_sum(o.y), sv = pair_sum(o.z);
-    cpb[oc] = su;
-    cpb[oc + 2 * CBH * CBW] = sv;
-  }
-  __syncthreads();
 
-  // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
-  const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + f * F.out_fp[0], (long long)H * F.out_ls[0]);
-  {
-    const int r = t >> 3, c = t & 7;
-    if (py0 + r < H) {
-      const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
-      const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
-      const int off = (py0 + r) * (int)F.out_ls[0];
-      if (F.out8)
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
-            oy_, off + px0 + 8 * c, 0, NT);
-      else
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
-            oy_, off + 2 * (px0 + 8 * c), 0, NT);
+  for (;;) {
+    // ---- commit this tile's registers to LDS ----
+    {
+      float v[8];
+      unpack8(cur.ya, v);
+      float* d = yin + (t >> 3) * YST + 8 * (t & 7);
+      const float ys = F.ys * (float)ESC;   // zimg depth-conversion scale
+      *reinterpret_cast<float4*>(d) = make_float4(v[0] * ys, v[1] * ys, v[2] * ys, v[3] * ys);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ys, v[5] * ys, v[6] * ys, v[7] * ys);
     }
-  }
-  if (t < 128) {
-    // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
-    const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
-    if (cy0 + r < ch) {
-      const float4* src = reinterpret_cast<const float4*>(cpair[pl] + r * CBW + 8 * c);
-      unsigned code[8];
+    if (t < 72) {
+      // horizontal pass (left siting, x2 scale): h[2k] = 2 c[k],
+      // h[2k+1] = c[k] + c[k+1]; exact in float
+      auto put = [&](const uint4 a, unsigned h, float* plane) {
+        float v[9];
+        unpack8(a, v);
+        v[8] = (float)h;
+        float* d = plane + (t >> 2) * HST + 16 * (t & 3);
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const float4 v = src[k];
-        code[2 * k] = (unsigned)(int)((v.x + v.y) + F.c_bias) << F.shift_out;
-        code[2 * k + 1] = (unsigned)(int)((v.z + v.w) + F.c_bias) << F.shift_out;
-      }
-      const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + f * F.out_fp[1 + pl], (long long)ch * F.out_ls[1 + pl]);
-      const int off = (cy0 + r) * (int)F.out_ls[1 + pl];
-      if (F.out8)
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
-                                               code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
-            oc_, off + cx0 + 8 * c, 0, NT);
-      else
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
-                                               code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
-            oc_, off + 2 * (cx0 + 8 * c), 0, NT);
+        for (int k = 0; k < 4; k++)
+          *reinterpret_cast<float4*>(d + 4 * k) =
+              make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
+      };
+      put(cur.ua, cur.uh, hrow[0]);
+      put(cur.va, cur.vh, hrow[1]);
     }
+    const TileGeo g = geo;
+    const bool more = tile + 1 < tend;   // block-uniform
+    if (more) {
+      geo = tile_geo(F, tile + 1);
+      cur = tile_load(F, geo, t);        // in flight during this tile's compute
+    }
+    __syncthreads();
+
+    // hot constants live in VGPRs
+    const float k_r = in_vgpr(F.k_r) * (float)ESC, k_g = in_vgpr(F.k_g) * (float)ESC, k_b = in_vgpr(F.k_b) * (float)ESC;
+    const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
+                a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
+    const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
+    const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
+    const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
+    const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
+      const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
+      const int oc = 2 * (4 * (s >> 1) * CBW + 4 * (s & 1));
+      const float ybs = ybase[oy];
+      const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
+      const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
+      const float er = fmaf(V, a_rv, ybs + k_r);
+      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + k_g));
+      const float eb = fmaf(U, a_bu, ybs + k_b);
+      float r, gg, bl;
+      to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
+      tone<TM, DESAT>(F, r, gg, bl);
+      // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
+      // s < N-1 and the lattice cell index never needs a clamp
+      const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+      const float sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+      const float sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+      const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
+      const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
+      const bool rg = dr > dg, gb = dg > db, rb = dr > db;
+      const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
+      const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
+      const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
+      const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
+      const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
+      const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0);
+      const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0);
+      const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0);
+      const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
+      const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
+      const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+      // luma code (eq applied, shifted) replaces the luma sample this lane read
+      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
+      // chroma: horizontal pair sums; both lanes of a pair store the same value
+      const float su = pair_sum(o.y), sv = pair_sum(o.z);
+      cpb[oc] = su;
+      cpb[oc + 2 * CBH * CBW] = sv;
+    }
+    __syncthreads();
+
+    // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
+    {
+      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], (long long)F.H * F.out_ls[0]);
+      const int r = t >> 3, c = t & 7;
+      if (g.py0 + r < F.H) {
+        const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
+        const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
+        const int off = (g.py0 + r) * (int)F.out_ls[0];
+        if (F.out8)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
+              oy_, off + g.px0 + 8 * c, 0, NT);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
+              oy_, off + 2 * (g.px0 + 8 * c), 0, NT);
+      }
+    }
+    if (t < 128) {
+      // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
+      const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
+      if (g.cy0 + r < F.ch) {
+        const float4* src = reinterpret_cast<const float4*>(cpair[pl] + r * CBW + 8 * c);
+        unsigned code[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float4 v = src[k];
+          code[2 * k] = (unsigned)(int)((v.x + v.y) + F.c_bias) << F.shift_out;
+          code[2 * k + 1] = (unsigned)(int)((v.z + v.w) + F.c_bias) << F.shift_out;
+        }
+        const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], (long long)F.ch * F.out_ls[1 + pl]);
+        const int off = (g.cy0 + r) * (int)F.out_ls[1 + pl];
+        if (F.out8)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
+                                                 code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
+              oc_, off + g.cx0 + 8 * c, 0, NT);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
+                                                 code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
+              oc_, off + 2 * (g.cx0 + 8 * c), 0, NT);
+      }
+    }
+    if (!more) break;
+    ++tile;
+    __syncthreads();   // the store phase has read yin / cpair before they are refilled
   }
 }
 
@@ -394,8 +454,9 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 7; }
 
 hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStream_t s) {
-  const long long nb = (long long)F.nbx * F.nby * F.nframes;
-  if (nb == 0) return hipSuccess;
+  const long long nt = (long long)F.nbx * F.nby * F.nframes;
+  if (nt == 0) return hipSuccess;
+  const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb), block(256);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7) desat = false;
