@@ -164,9 +164,12 @@ constexpr int YST = 68;            // LDS row stride (floats) of the luma tile
 constexpr int HST = 68;            // LDS row stride of the horizontally upsampled chroma rows
 constexpr int NT = 2;              // buffer-op aux bits: non-temporal (streamed frame bytes)
 
-__device__ __forceinline__ float pair_sum(float v) {
-  // v0 + v1 in both lanes of each horizontal pixel pair of a quad
-  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+__device__ __forceinline__ float quad_sum(float v) {
+  // (v0 + v1) + (v2 + v3) over the 2x2 pixels of a quad, in all 4 lanes
+  // (quad_perm [1,0,3,2] pairs horizontally, then [2,3,0,1] adds the rows):
+  // the oracle's summation order, so the chroma sum is bit-identical
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ void unpack8(const uint4 a, float* o) {
@@ -239,12 +242,15 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 // longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
 // barrier, 8 compute steps, barrier, store, barrier.
 template <int TRC, int TM, bool DESAT>
-// 5 waves per SIMD is the LDS-bound occupancy (5 blocks x 31 KB per CU): let
-// the compiler use the VGPRs that allows (<= 96), no more
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
+#ifndef H2S_WPE
+#define H2S_WPE 5
+#endif
+// H2S_WPE waves per SIMD = the LDS-bound occupancy (blocks of ~27 KB per
+// CU): let the compiler use the VGPRs that allows, no more
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_WPE))) void k_tile(const FastParams F) {
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
-  __shared__ float2 cpair[2][CBH * CBW];       // per chroma sample: (top pair sum, bottom pair sum)
+  __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG : 1];
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const float* h0 = hrow[0] + (qy + 1) * HST + xl;
   const float* h1 = hrow[1] + (qy + 1) * HST + xl;
   const int hb = pyl ? HST : -HST;
-  float* cpb = reinterpret_cast<float*>(cpair[0]) + 2 * (qy * CBW + 8 * w + qx) + pyl;
+  float* csb = csum[0] + qy * CBW + 8 * w + qx;
 
   for (;;) {
     // ---- commit this tile's registers to LDS ----
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     for (int s = 0; s < 8; s++) {
       const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
       const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
-      const int oc = 2 * (4 * (s >> 1) * CBW + 4 * (s & 1));
+      const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
       const float ybs = ybase[oy];
       const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
       const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
@@ -361,10 +367,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
-      // chroma: horizontal pair sums; both lanes of a pair store the same value
-      const float su = pair_sum(o.y), sv = pair_sum(o.z);
-      cpb[oc] = su;
-      cpb[oc + 2 * CBH * CBW] = sv;
+      // chroma: 2x2 sums; the 4 lanes of a quad store the same value
+      const float su = quad_sum(o.y), sv = quad_sum(o.z);
+      csb[oc] = su;
+      csb[oc + CBH * CBW] = sv;
     }
     __syncthreads();
 
@@ -390,14 +396,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
       const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
       if (g.cy0 + r < F.ch) {
-        const float4* src = reinterpret_cast<const float4*>(cpair[pl] + r * CBW + 8 * c);
+        const float4* src = reinterpret_cast<const float4*>(csum[pl] + r * CBW + 8 * c);
+        const float4 v0 = src[0], v1 = src[1];
+        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         unsigned code[8];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float4 v = src[k];
-          code[2 * k] = (unsigned)(int)((v.x + v.y) + F.c_bias) << F.shift_out;
-          code[2 * k + 1] = (unsigned)(int)((v.z + v.w) + F.c_bias) << F.shift_out;
-        }
+        for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
         const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], (long long)F.ch * F.out_ls[1 + pl]);
         const int off = (g.cy0 + r) * (int)F.out_ls[1 + pl];
         if (F.out8)
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
     if (!more) break;
     ++tile;
-    __syncthreads();   // the store phase has read yin / cpair before they are refilled
+    __syncthreads();   // the store phase has read yin / csum before they are refilled
   }
 }
 
@@ -460,9 +464,10 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStre
   dim3 grid((unsigned)nb), block(256);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7) desat = false;
+#define K_FAST k_tile
 #define X(T, M, D)                                                   \
   if (trc == T && tm == M && desat == D) {                           \
-    hipLaunchKernelGGL((k_tile<T, M, D>), grid, block, lds, s, F);   \
+    hipLaunchKernelGGL((K_FAST<T, M, D>), grid, block, lds, s, F);   \
     return hipGetLastError();                                        \
   }
   FAST_CASES(X)
