@@ -89,7 +89,7 @@ class Tonemapper:
             if path is None or path == '<LUT>':
                 self.set_lut(_lut.generate_lattice(_lut.LUT_SIZE))
             else:
-                self.load_cube(path.replace('\\\\:', ':'))
+                self.load_cube(_lut.unescape_filter_path(path))
         return params
 
     # ---- execution ----------------------------------------------------------

@@ -56,6 +56,12 @@ def parse_cube(text: 'str | bytes') -> np.ndarray:
     return out
 
 
+def unescape_filter_path(path: str) -> str:
+    """Inverse of the reference's _escape_path_for_filter (src/utils.py:188-204):
+    the drive colon was written as two backslashes + ':' for the filtergraph."""
+    return path.replace('\\\\:', ':').replace('\\:', ':')
+
+
 def load_cube(path: str) -> np.ndarray:
     if not os.path.exists(path):
         # src/utils.py:185-186
