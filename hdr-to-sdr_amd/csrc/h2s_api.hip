@@ -19,6 +19,11 @@ hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
 bool fast_supported(int tonemap);
 hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
+hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
+                            long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
+                            hipStream_t s);
+hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
+                             int w, int h, uint8_t* rgb, long long rls, const uint8_t* glut, hipStream_t s);
 }  // namespace h2s
 
 using h2s::FastParams;
@@ -44,6 +49,8 @@ struct h2s_ctx {
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
+  void* d_prev = nullptr;  // preview scratch
+  size_t prev_bytes = 0;
   std::string err;
   bool timing = false;
   hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
@@ -407,6 +414,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_eq) hipFree(c->d_eq);
   if (c->d_pq) hipFree(c->d_pq);
   if (c->d_stage) hipFree(c->d_stage);
+  if (c->d_prev) hipFree(c->d_prev);
   for (int i = 0; i < kEvRing; i++) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
@@ -687,6 +695,167 @@ int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb,
   if (din_mem) hipFree(din_mem);
   if (out_location == H2S_LOC_HOST) hipFree(dout);
   if (e != hipSuccess) return hip_fail(c, e, "debug kernel");
+  return 0;
+}
+
+// ---- preview ---------------------------------------------------------------
+
+int h2s_preview_size(int in_w, int in_h, int box_w, int box_h, int* out_w, int* out_h) {
+  if (in_w <= 0 || in_h <= 0 || box_w <= 0 || box_h <= 0 || !out_w || !out_h)
+    return fail(nullptr, H2S_E_INVALID_ARG, "preview sizes must be positive");
+  // libavfilter scale_eval: av_rescale (round half away from zero) of the
+  // box by the input aspect, then min with the box (decrease)
+  auto rescale = [](long long a, long long b, long long c) { return (a * b + c / 2) / c; };
+  const long long tw = rescale(box_h, in_w, in_h), th = rescale(box_w, in_h, in_w);
+  *out_w = (int)(tw < box_w ? tw : box_w);
+  *out_h = (int)(th < box_h ? th : box_h);
+  if (*out_w < 1) *out_w = 1;
+  if (*out_h < 1) *out_h = 1;
+  return 0;
+}
+
+namespace {
+// swscale SWS_BICUBIC with its default parameters B = 0, C = 0.6
+double bicubic(double x) {
+  const double B = 0.0, C = 0.6;
+  x = fabs(x);
+  if (x < 1.0) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) / 6.0;
+  if (x < 2.0) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) / 6.0;
+  return 0.0;
+}
+
+// per output index: first source tap and T normalised weights (centre-aligned
+// sampling; the kernel widens by the ratio when downscaling)
+int resize_taps(int src, int dst, std::vector<float>* w, std::vector<int>* start) {
+  const double scale = (double)src / dst, fw = scale > 1.0 ? scale : 1.0;
+  const int T = (int)ceil(4.0 * fw) + 1;
+  w->assign((size_t)dst * T, 0.0f);
+  start->assign(dst, 0);
+  for (int o = 0; o < dst; o++) {
+    const double c = (o + 0.5) * scale - 0.5;
+    const int s0 = (int)floor(c - 2.0 * fw) + 1;
+    double sum = 0.0, tmp[64];
+    for (int i = 0; i < T && i < 64; i++) sum += (tmp[i] = bicubic((s0 + i - c) / fw));
+    for (int i = 0; i < T && i < 64; i++) (*w)[(size_t)o * T + i] = (float)(tmp[i] / sum);
+    (*start)[o] = s0;
+  }
+  return T;
+}
+}  // namespace
+
+int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rgb_linesize, int out_w, int out_h,
+                      double display_gamma, int rgb_location, void* hip_stream) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (!rgb || out_w <= 0 || out_h <= 0 || rgb_linesize < 3LL * out_w)
+    return fail(c, H2S_E_INVALID_ARG, "bad RGB output geometry");
+  if (!(display_gamma > 0.0)) return fail(c, H2S_E_INVALID_ARG, "display gamma must be > 0");
+  if (!c->params_set) return fail(c, H2S_E_INVALID_ARG, "h2s_set_params was not called");
+  if (c->params.bits_out != 8)
+    return fail(c, H2S_E_INVALID_ARG, "preview needs params.bits_out == 8 (the chain's yuv420p)");
+  int rc = check_frames(c, in, c->params.bits_in, "input");
+  if (rc) return rc;
+  const int W = in->width, H = in->height;
+  const bool scale = out_w != W || out_h != H;
+  if (scale && (out_w > 4 * 8192 || out_h > 4 * 8192 || (double)W / out_w > 12.0 || (double)H / out_h > 12.0))
+    return fail(c, H2S_E_UNSUPPORTED, "preview resize ratio out of range");
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)hip_stream;
+  // scratch: chain output (yuv420p), resized planes, tap tables, RGB, gamma LUT
+  const int ow2 = (out_w + 1) / 2, oh2 = (out_h + 1) / 2;
+  std::vector<float> wx, wy, wcx, wcy;
+  std::vector<int> sx, sy, scx, scy;
+  int T = 0, Tc = 0;
+  if (scale) {
+    T = resize_taps(W, out_w, &wx, &sx);
+    const int Ty = resize_taps(H, out_h, &wy, &sy);
+    Tc = resize_taps(W / 2, ow2, &wcx, &scx);
+    const int Tcy = resize_taps(H / 2, oh2, &wcy, &scy);
+    if (Ty != T || Tcy != Tc) {  // one T per plane: recompute on the wider support
+      const int Tm = T > Ty ? T : Ty, Tcm = Tc > Tcy ? Tc : Tcy;
+      auto widen = [](std::vector<float>* w, int n, int t, int tn) {
+        std::vector<float> o((size_t)n * tn, 0.0f);
+        for (int i = 0; i < n; i++)
+          for (int k = 0; k < t; k++) o[(size_t)i * tn + k] = (*w)[(size_t)i * t + k];
+        *w = o;
+      };
+      if (T < Tm) widen(&wx, out_w, T, Tm);
+      if (Ty < Tm) widen(&wy, out_h, Ty, Tm);
+      if (Tc < Tcm) widen(&wcx, ow2, Tc, Tcm);
+      if (Tcy < Tcm) widen(&wcy, oh2, Tcy, Tcm);
+      T = Tm, Tc = Tcm;
+    }
+  }
+  uint8_t glut[256];
+  for (int i = 0; i < 256; i++) {
+    // PIL point() with round() of pow(i/255, 1/gamma)*255 (round half to even)
+    const double v = display_gamma == 1.0 ? (double)i : pow(i / 255.0, 1.0 / display_gamma) * 255.0;
+    const double r = nearbyint(v);
+    glut[i] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+  }
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t yuv_b = al((size_t)W * H * 3 / 2), syuv_b = scale ? al((size_t)out_w * out_h + 2 * (size_t)ow2 * oh2) : 0;
+  const size_t tab_b = scale ? al((wx.size() + wy.size() + wcx.size() + wcy.size()) * 4) +
+                                   al((sx.size() + sy.size() + scx.size() + scy.size()) * 4)
+                             : 0;
+  const size_t rgb_b = rgb_location == H2S_LOC_HOST ? al((size_t)out_w * 3 * out_h) : 0;
+  const size_t need = yuv_b + syuv_b + tab_b + rgb_b + 256;
+  if (need > c->prev_bytes) {
+    if (c->d_prev) hipFree(c->d_prev);
+    c->d_prev = nullptr;
+    c->prev_bytes = 0;
+    if (hipMalloc(&c->d_prev, need) != hipSuccess) {
+      c->d_prev = nullptr;
+      return fail(c, H2S_E_OOM, "preview scratch allocation failed");
+    }
+    c->prev_bytes = need;
+  }
+  uint8_t* base = (uint8_t*)c->d_prev;
+  h2s_frames y8{};
+  y8.width = W, y8.height = H, y8.bits = 8, y8.location = H2S_LOC_DEVICE;
+  y8 = tight(&y8, base);
+  if ((rc = h2s_process(c, in, &y8, 1, hip_stream))) return rc;
+  hipError_t e = hipSuccess;
+  const uint8_t *yp = (const uint8_t*)y8.data[0], *up = (const uint8_t*)y8.data[1], *vp = (const uint8_t*)y8.data[2];
+  long long yls = W, cls = W / 2;
+  uint8_t* p = base + yuv_b;
+  if (scale) {
+    uint8_t* sy_ = p;
+    uint8_t* su_ = p + (size_t)out_w * out_h;
+    uint8_t* sv_ = su_ + (size_t)ow2 * oh2;
+    uint8_t* t = p + syuv_b;
+    float* dwx = (float*)t;
+    float* dwy = dwx + wx.size();
+    float* dwcx = dwy + wy.size();
+    float* dwcy = dwcx + wcx.size();
+    int* dsx = (int*)(t + al((wx.size() + wy.size() + wcx.size() + wcy.size()) * 4));
+    int* dsy = dsx + sx.size();
+    int* dscx = dsy + sy.size();
+    int* dscy = dscx + scx.size();
+    struct {
+      void* d;
+      const void* h;
+      size_t b;
+    } up_[8] = {{dwx, wx.data(), wx.size() * 4},   {dwy, wy.data(), wy.size() * 4},   {dwcx, wcx.data(), wcx.size() * 4},
+                {dwcy, wcy.data(), wcy.size() * 4}, {dsx, sx.data(), sx.size() * 4},   {dsy, sy.data(), sy.size() * 4},
+                {dscx, scx.data(), scx.size() * 4}, {dscy, scy.data(), scy.size() * 4}};
+    for (auto& u : up_)
+      if (e == hipSuccess) e = hipMemcpyAsync(u.d, u.h, u.b, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = h2s::launch_resize_u8(yp, W, H, W, sy_, out_w, out_h, out_w, dwx, dsx, dwy, dsy, T, s);
+    if (e == hipSuccess)
+      e = h2s::launch_resize_u8(up, W / 2, H / 2, W / 2, su_, ow2, oh2, ow2, dwcx, dscx, dwcy, dscy, Tc, s);
+    if (e == hipSuccess)
+      e = h2s::launch_resize_u8(vp, W / 2, H / 2, W / 2, sv_, ow2, oh2, ow2, dwcx, dscx, dwcy, dscy, Tc, s);
+    yp = sy_, up = su_, vp = sv_, yls = out_w, cls = ow2;
+  }
+  uint8_t* dglut = base + need - 256;
+  uint8_t* drgb = rgb_location == H2S_LOC_HOST ? base + yuv_b + syuv_b + tab_b : rgb;
+  const long long drls = rgb_location == H2S_LOC_HOST ? 3LL * out_w : rgb_linesize;
+  if (e == hipSuccess) e = hipMemcpyAsync(dglut, glut, 256, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = h2s::launch_yuv8_rgb24(yp, yls, up, vp, cls, out_w, out_h, drgb, drls, dglut, s);
+  if (e == hipSuccess && rgb_location == H2S_LOC_HOST)
+    e = hipMemcpy2DAsync(rgb, rgb_linesize, drgb, drls, 3 * (size_t)out_w, out_h, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(c, e, "preview");
   return 0;
 }
 

@@ -172,6 +172,24 @@ int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
 int h2s_debug_float(h2s_ctx *ctx, const h2s_frames *in, int stage,
                     float *out_rgb, int out_location, void *hip_stream);
 
+/* ---- preview (src/utils.py:719-765 extract_frame_with_conversion, the
+ * GUI's adjust_gamma src/preview.py:108-117) ------------------------------
+ * h2s_preview_size: the size FFMPEG_FILTER's trailing
+ *   scale=W:H:force_original_aspect_ratio=decrease (src/utils.py:46-49) gives
+ *   an in_w x in_h frame in a box_w x box_h box (PREVIEW_SIZE = 3840x2160,
+ *   src/preview.py:29); upscales too, as ffmpeg's scale does.
+ * h2s_preview_rgb24: frame 0 of `in` through the chain (ctx params; bits_out
+ *   must be 8: the yuv420p the PNG encoder reads), the bicubic (B=0, C=0.6)
+ *   resize to out_w x out_h when that differs from the frame size, BT.709
+ *   limited Y'CbCr -> full-range RGB24 (nearest chroma), then the display
+ *   gamma LUT round(255 (i/255)^(1/gamma)) on R, G, B (1.0 = identity).
+ *   rgb: out_h rows of out_w*3 bytes, rgb_linesize apart, host or device per
+ *   rgb_location.  Synchronous. */
+int h2s_preview_size(int in_w, int in_h, int box_w, int box_h, int *out_w, int *out_h);
+int h2s_preview_rgb24(h2s_ctx *ctx, const h2s_frames *in, uint8_t *rgb, int64_t rgb_linesize,
+                      int out_w, int out_h, double display_gamma, int rgb_location,
+                      void *hip_stream);
+
 /* ---- .cube helpers (tools/generate_lut.py:28-119; lut3d's .cube parser) --
  * h2s_cube_generate: the BT.2020->BT.709 lattice, n^3 triples, .cube order,
  *   rounded exactly as the "%.6f" text the reference writes, then parsed to

@@ -102,6 +102,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_pq_eotf.argtypes = [ctypes.c_float]
         L.oracle_hlg_inverse_oetf.restype = ctypes.c_float
         L.oracle_hlg_inverse_oetf.argtypes = [ctypes.c_float]
+        L.oracle_preview_tail.restype = ctypes.c_int
+        L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -154,6 +157,20 @@ def debug_float(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, w
                                   ctypes.byref(din), stage, out.ctypes.data)
     if rc:
         raise ValueError(f'oracle_debug_float failed: {rc}')
+    return out
+
+
+def preview_rgb24(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
+                  out_w: int, out_h: int, gamma: float = 1.0) -> np.ndarray:
+    """Preview of frame 0: the chain at bits_out 8, then the restated scale /
+    yuv420p->rgb24 / adjust_gamma tail (PARITY UNPINNED, see h2s_oracle.c)."""
+    if params.bits_out != 8:
+        raise ValueError('preview runs the chain at bits_out 8')
+    yuv8 = np.ascontiguousarray(process(params, lattice, np.ascontiguousarray(buf[:1]), width, height)[0])
+    out = np.zeros((out_h, out_w, 3), dtype=np.uint8)
+    rc = lib().oracle_preview_tail(yuv8.ctypes.data, width, height, out_w, out_h, float(gamma), out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_preview_tail failed: {rc}')
     return out
 
 

@@ -577,3 +577,84 @@ float oracle_tone_curve(const h2s_params *p, float sig) {
 
 float oracle_pq_eotf(float x) { return st2084_eotf(x); }
 float oracle_hlg_inverse_oetf(float x) { return arib_b67_inverse_oetf(x); }
+
+/* ---- preview tail (src/utils.py:46-49 FFMPEG_FILTER's scale=..., the PNG
+ * encoder's yuv420p -> rgb24, src/preview.py:108-117 adjust_gamma) --------
+ * PARITY UNPINNED: no ffmpeg/swscale here; this is the restated model the
+ * GPU preview follows: swscale SWS_BICUBIC (B=0, C=0.6), centre-aligned,
+ * support widened by the ratio when downscaling, edge-clamped; BT.709
+ * limited -> full-range RGB with nearest chroma; PIL's round-half-even LUT. */
+static double o_bicubic(double x) {
+  const double B = 0.0, C = 0.6;
+  x = fabs(x);
+  if (x < 1.0) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) / 6.0;
+  if (x < 2.0) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) / 6.0;
+  return 0.0;
+}
+
+static void o_resize(const uint8_t *src, int sw, int sh, uint8_t *dst, int ow, int oh) {
+  const double scx = (double)sw / ow, scy = (double)sh / oh;
+  const double fx = scx > 1 ? scx : 1, fy = scy > 1 ? scy : 1;
+  for (int y = 0; y < oh; y++) {
+    const double cy = (y + 0.5) * scy - 0.5;
+    const int y0 = (int)floor(cy - 2 * fy) + 1, ty = (int)ceil(4 * fy) + 1;
+    for (int x = 0; x < ow; x++) {
+      const double cx = (x + 0.5) * scx - 0.5;
+      const int x0 = (int)floor(cx - 2 * fx) + 1, tx = (int)ceil(4 * fx) + 1;
+      double acc = 0, swy = 0;
+      for (int j = 0; j < ty; j++) {
+        const double wyj = o_bicubic((y0 + j - cy) / fy);
+        swy += wyj;
+        int r = y0 + j;
+        r = r < 0 ? 0 : (r > sh - 1 ? sh - 1 : r);
+        double h = 0, swx = 0;
+        for (int i = 0; i < tx; i++) {
+          const double wxi = o_bicubic((x0 + i - cx) / fx);
+          swx += wxi;
+          int c = x0 + i;
+          c = c < 0 ? 0 : (c > sw - 1 ? sw - 1 : c);
+          h += wxi * src[(size_t)r * sw + c];
+        }
+        acc += wyj * h / swx;
+      }
+      const double v = floor(acc / swy + 0.5);
+      dst[(size_t)y * ow + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+  }
+}
+
+/* yuv8: one tight yuv420p frame (W x H) as the chain produced it */
+int oracle_preview_tail(const uint8_t *yuv8, int W, int H, int ow, int oh, double gamma, uint8_t *rgb) {
+  const int cw = W / 2, ch = H / 2, ow2 = (ow + 1) / 2, oh2 = (oh + 1) / 2;
+  const uint8_t *Y = yuv8, *U = yuv8 + (size_t)W * H, *V = U + (size_t)cw * ch;
+  uint8_t *tmp = NULL;
+  int yw = W, cws = cw;
+  if (ow != W || oh != H) {
+    tmp = (uint8_t *)malloc((size_t)ow * oh + 2 * (size_t)ow2 * oh2);
+    if (!tmp) return H2S_E_OOM;
+    o_resize(Y, W, H, tmp, ow, oh);
+    o_resize(U, cw, ch, tmp + (size_t)ow * oh, ow2, oh2);
+    o_resize(V, cw, ch, tmp + (size_t)ow * oh + (size_t)ow2 * oh2, ow2, oh2);
+    Y = tmp, U = tmp + (size_t)ow * oh, V = U + (size_t)ow2 * oh2, yw = ow, cws = ow2;
+  }
+  uint8_t lut[256];
+  for (int i = 0; i < 256; i++) {
+    const double v = gamma == 1.0 ? i : pow(i / 255.0, 1.0 / gamma) * 255.0;
+    const double r = nearbyint(v); /* Python round(): half to even */
+    lut[i] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+  }
+  for (int y = 0; y < oh; y++)
+    for (int x = 0; x < ow; x++) {
+      const double yy = 255.0 / 219.0 * (Y[(size_t)y * yw + x] - 16.0);
+      const double u = U[(size_t)(y / 2) * cws + x / 2] - 128.0, v = V[(size_t)(y / 2) * cws + x / 2] - 128.0;
+      const double kr = 0.2126, kb = 0.0722, kg = 1 - kr - kb, cs = 255.0 / 224.0;
+      const double c[3] = {yy + 2 * (1 - kr) * cs * v, yy - 2 * kb * (1 - kb) / kg * cs * u - 2 * kr * (1 - kr) / kg * cs * v,
+                           yy + 2 * (1 - kb) * cs * u};
+      for (int k = 0; k < 3; k++) {
+        const double q = floor(c[k] + 0.5);
+        rgb[((size_t)y * ow + x) * 3 + k] = lut[(int)(q < 0 ? 0 : (q > 255 ? 255 : q))];
+      }
+    }
+  free(tmp);
+  return 0;
+}

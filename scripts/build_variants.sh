@@ -12,7 +12,7 @@ for spec in "$@"; do
   [ "$flags" = "$spec" ] && flags=""
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -shared -fPIC \
     -Wno-unused-value -Wno-unused-result $flags -o "$ROOT/scripts/variants/libh2s_$name.so" \
-    "$C/h2s_api.hip" "$C/h2s_kernels.hip" "$C/h2s_fast.hip" "$C/h2s_cube.cpp" &
+    "$C/h2s_api.hip" "$C/h2s_kernels.hip" "$C/h2s_fast.hip" "$C/h2s_preview.hip" "$C/h2s_cube.cpp" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
