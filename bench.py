@@ -103,10 +103,16 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # one process per GPU; H2S_BENCH_DEVICE / H2S_DIST_BACKEND=gloo only let a
+    # single-GPU box rehearse the multi-rank flow (ranks sharing one device)
+    local = int(os.environ.get('H2S_BENCH_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+    backend = os.environ.get('H2S_DIST_BACKEND', 'nccl')
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
