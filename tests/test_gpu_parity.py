@@ -193,3 +193,24 @@ def test_errors_map_to_reference_exceptions(tm):
     with pytest.raises(FileNotFoundError):
         fresh(src)
     fresh.close()
+
+
+# ---- BASELINE.json full sizes (the oracle is OpenMP C: whole frames in ~1 s)
+@pytest.mark.parametrize('name,kw,W,H,nframes', [
+    ('C2_4k_hable_g22', dict(tonemapper='hable', gamma=2.2, bits_out=10), 3840, 2160, 2),
+    ('C3_4k_bt2390', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('C4_4k_mobius', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('C5_8k_hlg12_hable', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
+     7680, 4320, 1),
+    ('C1_1080p_reinhard_8bit', dict(tonemapper='reinhard', gamma=1.0, bits_out=8), 1920, 1080, 1),
+])
+def test_full_size_configs(tm, name, kw, W, H, nframes):
+    params = hdr2sdr.TonemapParams(**kw)
+    got, want, _ = run_both(tm, params, 'smooth', W, H, nframes=nframes, lut_n=33 if name.startswith('C1') else 65)
+    assert_close_int(params, got, want, W, H)
+
+
+def test_full_size_uniform_worst_case(tm):
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=10)
+    got, want, _ = run_both(tm, params, 'uniform', 3840, 2160, nframes=1)
+    assert_close_int(params, got, want, 3840, 2160)
