@@ -90,13 +90,8 @@ struct FastParams {
 };
 
 constexpr int PQ_SEG = 128;          // segments per unit of E
-#ifdef H2S_PQ192
-constexpr int PQ_NSEG = 192;         // table covers E in [0, 1.5)
-constexpr float PQ_EMAX = 1.5f;      // above: exact transcendental path
-#else
 constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
 constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
-#endif
 
 struct YuvLutConsts {
   float s, k709[3], kcb[3], kcr[3];

@@ -2,9 +2,8 @@
 //
 // Same chain as k_generic (h2s_kernels.hip) and oracle/h2s_oracle.c, restated
 // for throughput on gfx950:
-//  * one template instance per (transfer, operator, desat) so the 16 pixels a
-//    work item owns are straight-line code the compiler can interleave (the
-//    v1 kernel's per-pixel uniform branches serialised every LUT gather);
+//  * one template instance per (transfer, operator, desat): the 8 steps a wave
+//    runs per tile are straight-line code the compiler can interleave;
 //  * chroma upsampling on integer-valued floats (exact), the 1/4, 1/8 and
 //    depth-normalisation scales folded into the Y'CbCr->R'G'B' constants;
 //  * the 3D-LUT lattice pre-multiplied into output Y'CbCr code space
@@ -13,14 +12,15 @@
 //    tetrahedral blend then yields quantiser inputs directly;
 //  * lattice gathers are buffer loads (32-bit offsets, one SGPR base);
 //  * eq's table sits in LDS.
-// Geometry (k_tile): a block of 256 threads owns a 64 x 32 luma tile of one
-// frame.  The tile (Y, and U/V with their 1-sample halo) is staged into LDS
-// with coalesced 16-byte loads; then, in 8 steps, each wave processes one
-// dense 8 x 8 pixel sub-block with one pixel per lane (lanes 4q..4q+3 = one
-// 2x2 quad).  Dense sub-blocks keep the 64 lanes of every lattice gather on
-// few cache lines (the gathers, not the arithmetic, bound this kernel);
+// Geometry (k_tile): a block of 256 threads walks 8 consecutive 64 x 32 luma
+// tiles, prefetching tile i+1 into registers while tile i computes.  A tile
+// (Y, and U/V with their 1-row halo) is staged into LDS with coalesced
+// 16-byte loads; then, in 8 steps, each wave processes one dense 8 x 8 pixel
+// sub-block with one pixel per lane (lanes 4q..4q+3 = one 2x2 quad).  Dense
+// sub-blocks keep the 64 lanes of every lattice gather on few cache lines;
 // chroma is reduced per quad with DPP quad permutes and all outputs leave
-// through LDS as 16-byte coalesced stores.
+// through LDS as 16-byte coalesced stores.  Measured balance (DESIGN.md
+// §4.1): VALU ~70 % busy, LDS ~47 %, vector-memory return ~35 %.
 #include <hip/hip_runtime.h>
 
 #include "h2s_device.h"
@@ -242,12 +242,9 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 // longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
 // barrier, 8 compute steps, barrier, store, barrier.
 template <int TRC, int TM, bool DESAT>
-#ifndef H2S_WPE
-#define H2S_WPE 5
-#endif
-// H2S_WPE waves per SIMD = the LDS-bound occupancy (blocks of ~27 KB per
-// CU): let the compiler use the VGPRs that allows, no more
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_WPE))) void k_tile(const FastParams F) {
+// 5 waves per SIMD = the LDS-bound occupancy (5 blocks of ~27.6 KB per CU;
+// 3 and 6 measured slower): let the compiler use the VGPRs that allows
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
