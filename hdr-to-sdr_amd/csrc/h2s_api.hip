@@ -24,6 +24,8 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, u
                             hipStream_t s);
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
                              int w, int h, uint8_t* rgb, long long rls, const uint8_t* glut, hipStream_t s);
+constexpr int PEAK_BLOCKS = 64;  // partial (max, sum) records per frame
+hipError_t launch_peak_stats(const KParams& P, float2* partial, hipStream_t s);
 }  // namespace h2s
 
 using h2s::FastParams;
@@ -51,6 +53,11 @@ struct h2s_ctx {
   size_t stage_bytes = 0;
   void* d_prev = nullptr;  // preview scratch
   size_t prev_bytes = 0;
+  // dynamic peak (params.peak_detect): per-frame stats buffer + IIR state
+  float2* d_peak = nullptr;
+  size_t peak_cap = 0;
+  double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
+  long long pk_frames = 0;
   std::string err;
   bool timing = false;
   hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
@@ -110,6 +117,29 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
   if (!(p->npl > 0) || !isfinite(p->npl)) return fail(c, H2S_E_INVALID_ARG, "npl must be > 0");
   if (!(p->desat >= 0)) return fail(c, H2S_E_INVALID_ARG, "desat must be >= 0");
   return 0;
+}
+
+// BT.2390 EETF constants for a source peak (units of 100 nits) and target npl
+void bt2390_consts(double peak, double npl, KParams* k) {
+  const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
+  const double ml = (pq_encode_d(npl / 10000.0) - smin) / (smax - smin);
+  const double ks = 1.5 * ml - 0.5;
+  k->b_srcmin = (float)smin;
+  k->b_range = (float)(smax - smin);
+  k->b_inv_range = (float)(1.0 / (smax - smin));
+  k->b_ks = (float)ks;
+  k->b_inv_1mks = (float)(1.0 / (1.0 - ks));
+  k->b_maxlum = (float)ml;
+}
+
+// ST 2084 EOTF in double (normalised: 1.0 = 10000 nits)
+double pq_eotf_d(double e) {
+  const double m1 = 2610.0 / 16384.0, m2 = 2523.0 / 4096.0 * 128.0, c1 = 3424.0 / 4096.0, c2 = 2413.0 / 4096.0 * 32.0,
+               c3 = 2392.0 / 4096.0 * 32.0;
+  if (!(e > 0.0)) return 0.0;
+  const double xp = pow(e, 1.0 / m2);
+  const double num = xp - c1 > 0.0 ? xp - c1 : 0.0;
+  return pow(num / (c2 - c3 * xp), 1.0 / m1);
 }
 
 void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
@@ -173,17 +203,8 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
     k->mob_j = j, k->mob_a = a, k->mob_b = b;
     k->mob_k = (b * b + 2.0f * b * j + j * j) / (b - a);
   }
-  {
-    const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
-    const double ml = (pq_encode_d(p->npl / 10000.0) - smin) / (smax - smin);
-    const double ks = 1.5 * ml - 0.5;
-    k->b_srcmin = (float)smin;
-    k->b_range = (float)(smax - smin);
-    k->b_inv_range = (float)(1.0 / (smax - smin));
-    k->b_ks = (float)ks;
-    k->b_inv_1mks = (float)(1.0 / (1.0 - ks));
-    k->b_maxlum = (float)ml;
-  }
+  k->peak = peak;
+  bt2390_consts(peak, p->npl, k);
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / p->npl);
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
@@ -415,6 +436,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_pq) hipFree(c->d_pq);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
+  if (c->d_peak) hipFree(c->d_peak);
   for (int i = 0; i < kEvRing; i++) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
@@ -480,6 +502,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   c->params = *p;
   c->k = k;
   c->params_set = true;
+  h2s_peak_reset(c);  // a new parameter set starts a new sequence
   return 0;
 }
 
@@ -571,6 +594,103 @@ static int prepare(h2s_ctx* c, KParams* k) {
   return 0;
 }
 
+// one launch of the chain over nframes frames described by k
+static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
+                               hipStream_t s) {
+  if (!fast) return h2s::launch_process(k, vec, out8, s);
+  FastParams F;
+  resolve_fast(c, k, &F);
+  for (int p = 0; p < 3; p++) {
+    F.in[p] = k.in[p], F.in_ls[p] = k.in_ls[p], F.in_fp[p] = k.in_fp[p];
+    F.out[p] = k.out[p], F.out_ls[p] = k.out_ls[p], F.out_fp[p] = k.out_fp[p];
+  }
+  F.W = k.W, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
+  F.nbx = (unsigned)(k.W / 64);
+  F.nby = (unsigned)((k.H + 31) / 32);
+  F.nframes = (unsigned)nframes;
+  F.tpb = c->tiles_per_block;
+  return h2s::launch_fast(F, k.transfer, k.tonemap, k.desat_on != 0, s);
+}
+
+// libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):
+// IIR low-pass with time constant 20 frames on the PQ-domain frame max and
+// average, bypassed progressively for scene changes whose average moves by
+// 10..30 % PQ (smoothstep); the result is clamped to [1, static peak].
+static double peak_update(h2s_ctx* c, double fmax, double favg, double static_peak) {
+  if (c->pk_frames == 0) {
+    c->pk_max = fmax, c->pk_avg = favg;
+  } else {
+    const double a = 1.0 - exp(-1.0 / 20.0);
+    double t = (fabs(favg - c->pk_avg) * 100.0 - 10.0) / 20.0;
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    const double w = a + (1.0 - a) * t * t * (3.0 - 2.0 * t);
+    c->pk_max += w * (fmax - c->pk_max);
+    c->pk_avg += w * (favg - c->pk_avg);
+  }
+  c->pk_frames++;
+  double peak = pq_eotf_d(c->pk_max) * 100.0;  // units of 100 nits, as vf_tonemap's peak
+  if (peak < 1.0) peak = 1.0;
+  if (peak > static_peak) peak = static_peak;
+  c->pk_peak = peak;
+  return peak;
+}
+
+// statistics for every frame in one launch, then the frames in order, each
+// with the BT.2390 constants of its smoothed peak
+static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
+  const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
+  if (need > c->peak_cap) {
+    if (c->d_peak) hipFree(c->d_peak);
+    c->d_peak = nullptr;
+    c->peak_cap = 0;
+    if (hipMalloc((void**)&c->d_peak, need * sizeof(float2)) != hipSuccess) {
+      c->d_peak = nullptr;
+      return fail(c, H2S_E_OOM, "peak statistics allocation failed");
+    }
+    c->peak_cap = need;
+  }
+  hipError_t e = h2s::launch_peak_stats(k, c->d_peak, s);
+  std::vector<float2> part(need);
+  if (e == hipSuccess) e = hipMemcpyAsync(part.data(), c->d_peak, need * sizeof(float2), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
+  const double npx = (double)k.W * k.H;
+  for (int f = 0; f < nframes; f++) {
+    double fmax = 0.0, fsum = 0.0;
+    for (int b = 0; b < h2s::PEAK_BLOCKS; b++) {
+      const float2 v = part[(size_t)f * h2s::PEAK_BLOCKS + b];
+      fmax = v.x > fmax ? v.x : fmax;
+      fsum += v.y;
+    }
+    KParams kf = k;
+    bt2390_consts(peak_update(c, fmax, fsum / npx, k.peak), c->params.npl, &kf);
+    for (int p = 0; p < 3; p++) {
+      kf.in[p] += f * kf.in_fp[p];
+      kf.out[p] += f * kf.out_fp[p];
+    }
+    kf.nframes = 1;
+    kf.total = (long long)kf.ch * kf.ngx;
+    if ((e = launch_chain(c, kf, fast, vec, out8, 1, s)) != hipSuccess) return hip_fail(c, e, "kernel launch");
+  }
+  return 0;
+}
+
+int h2s_peak_reset(h2s_ctx* c) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  c->pk_max = c->pk_avg = c->pk_peak = 0.0;
+  c->pk_frames = 0;
+  return 0;
+}
+
+int h2s_peak_state(const h2s_ctx* c, double* max_pq, double* avg_pq, double* peak, int64_t* frames) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (max_pq) *max_pq = c->pk_max;
+  if (avg_pq) *avg_pq = c->pk_avg;
+  if (peak) *peak = c->pk_peak;
+  if (frames) *frames = c->pk_frames;
+  return 0;
+}
+
 int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nframes, void* hip_stream) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (nframes < 0) return fail(c, H2S_E_INVALID_ARG, "nframes < 0");
@@ -626,21 +746,11 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     hipEventRecord(c->ev0[slot], s);
   }
   hipError_t e;
-  if (fast) {
-    FastParams F;
-    resolve_fast(c, k, &F);
-    for (int p = 0; p < 3; p++) {
-      F.in[p] = k.in[p], F.in_ls[p] = k.in_ls[p], F.in_fp[p] = k.in_fp[p];
-      F.out[p] = k.out[p], F.out_ls[p] = k.out_ls[p], F.out_fp[p] = k.out_fp[p];
-    }
-    F.W = k.W, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
-    F.nbx = (unsigned)(k.W / 64);
-    F.nby = (unsigned)((k.H + 31) / 32);
-    F.nframes = (unsigned)nframes;
-    F.tpb = c->tiles_per_block;
-    e = h2s::launch_fast(F, k.transfer, k.tonemap, k.desat_on != 0, s);
+  if (c->params.peak_detect && k.tonemap == H2S_TM_BT2390) {
+    if ((rc = run_dynamic_peak(c, k, fast, vec, out8, nframes, s))) return rc;
+    e = hipSuccess;
   } else {
-    e = h2s::launch_process(k, vec, out8, s);
+    e = launch_chain(c, k, fast, vec, out8, nframes, s);
   }
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   if (c->timing) {

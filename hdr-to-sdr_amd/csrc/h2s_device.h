@@ -38,6 +38,7 @@ struct KParams {
   float mob_j, mob_a, mob_b, mob_k;  // MOBIUS
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum;  // BT2390
   float npl_1e4, e4_npl;  // npl/10000, 10000/npl
+  double peak;            // resolved static source peak (units of 100 nits; host side)
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
   float lut_max;

@@ -253,4 +253,61 @@ hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s) 
   return hipGetLastError();
 }
 
+// ---- dynamic peak statistics (params.peak_detect, BT.2390) -----------------
+// Per frame, the maximum and the sum of the PQ-encoded max(R,G,B) of every
+// pixel (libplacebo peak detection, src/utils.py:448; PARITY UNPINNED: no
+// libplacebo here, model in DESIGN.md).  PQ sources: PQ(max(EOTF(E))) ==
+// clamp(max(E), 0, 1) exactly, so no transcendental is needed.  Chroma is
+// taken nearest (the statistic is an estimate).  grid = (PEAK_BLOCKS, frames);
+// partial[f * PEAK_BLOCKS + b] = (max, sum) over the rows b, b + PEAK_BLOCKS, ...
+template <int TRC>
+__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial) {
+  const int f = blockIdx.y, b = blockIdx.x;
+  float mx = 0.0f, sm = 0.0f;
+  for (int y = b; y < P.H; y += gridDim.x) {
+    const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
+    const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
+    const uint16_t* vr = reinterpret_cast<const uint16_t*>(P.in[2] + f * P.in_fp[2] + (y >> 1) * P.in_ls[2]);
+    float rs = 0.0f;
+    for (int x = threadIdx.x; x < P.W; x += blockDim.x) {
+      const float Y = (float)yr[x] * P.y_scale + P.y_off;
+      const float cb = (float)ur[x >> 1] * P.c_scale + P.c_off, cr = (float)vr[x >> 1] * P.c_scale + P.c_off;
+      const float er = Y + P.m_rcr * cr, eg = Y + P.m_gcb * cb + P.m_gcr * cr, eb = Y + P.m_bcb * cb;
+      float m;
+      if (TRC == 0) {
+        m = clamp01(fmaxf(fmaxf(er, eg), eb));
+      } else {
+        const float r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), bl = hlg_inv_oetf(eb);
+        const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * bl;
+        const float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
+        m = clamp01(pq_encode(fmaxf(fmaxf(r, g), bl) * w * P.npl_1e4));
+      }
+      mx = fmaxf(mx, m);
+      rs += m;
+    }
+    sm += rs;
+  }
+  __shared__ float smx[256], ssm[256];
+  smx[threadIdx.x] = mx, ssm[threadIdx.x] = sm;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + o]);
+      ssm[threadIdx.x] += ssm[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[f * gridDim.x + b] = make_float2(smx[0], ssm[0]);
+}
+
+constexpr int PEAK_BLOCKS_K = 64;
+hipError_t launch_peak_stats(const KParams& P, float2* partial, hipStream_t s) {
+  const dim3 grid(PEAK_BLOCKS_K, P.nframes);
+  if (P.transfer == 1)
+    hipLaunchKernelGGL(k_peak_stats<1>, grid, dim3(256), 0, s, P, partial);
+  else
+    hipLaunchKernelGGL(k_peak_stats<0>, grid, dim3(256), 0, s, P, partial);
+  return hipGetLastError();
+}
+
 }  // namespace h2s

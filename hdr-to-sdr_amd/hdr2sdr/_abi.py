@@ -34,7 +34,8 @@ EXPORTS = (
     'h2s_abi_version', 'h2s_create', 'h2s_destroy', 'h2s_last_error',
     'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
     'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
-    'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24',
+    'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_peak_reset',
+    'h2s_peak_state',
 )
 
 
@@ -54,7 +55,8 @@ class H2SParams(ctypes.Structure):
         ('lut_enabled', ctypes.c_int32),
         ('mode', ctypes.c_int32),
         ('desat_luma', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 5),
+        ('peak_detect', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 4),
     ]
 
 
@@ -133,6 +135,9 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]),
         'h2s_kernel_ms': (ctypes.c_double, [c_ctx, ctypes.c_int]),
         'h2s_set_timing': (ctypes.c_int, [c_ctx, ctypes.c_int]),
+        'h2s_peak_reset': (ctypes.c_int, [c_ctx]),
+        'h2s_peak_state': (ctypes.c_int, [c_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
         'h2s_preview_size': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
         'h2s_preview_rgb24': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_void_p, ctypes.c_int64,

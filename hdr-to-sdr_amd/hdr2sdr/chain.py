@@ -77,6 +77,7 @@ class TonemapParams:
     maxcll: float = 0.0
     mastering_max: float = 0.0
     desat_luma: str = 'rgb'
+    peak_detect: bool = False   # BT.2390: detected, smoothed per-frame peak (libplacebo peak_detect=1)
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
@@ -137,6 +138,7 @@ class TonemapParams:
         p.lut_enabled = 1 if self.lut_enabled else 0
         p.mode = _MODES[self.mode]
         p.desat_luma = _DESAT_LUMA[self.desat_luma]
+        p.peak_detect = 1 if self.peak_detect else 0
         return p
 
     # ---- back to the reference's chain string --------------------------
@@ -223,15 +225,17 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             kw['lut_enabled'] = True
         elif name == 'libplacebo':
             # GPU chain build_libplacebo_filter (src/utils.py:392-471): the
-            # tone map runs here natively.  libplacebo's own gamut/desat
-            # handling and peak_detect=1 (dynamic, temporally smoothed peak)
-            # are replaced by the static-peak operator: documented deviation.
+            # tone map runs here natively; libplacebo's own gamut/desat
+            # handling is replaced by the lut3d stage that follows it.
             tm = kv.get('tonemapping')
             if tm is None:
                 raise ValueError('libplacebo stage without tonemapping=')
             seen_linear = True
             kw['tonemapper'] = tm.lower()
             kw['desat'] = 0.0
+            # peak_detect=1 (src/utils.py:448): per-frame detected, temporally
+            # smoothed source peak; libh2s restates it for BT.2390
+            kw['peak_detect'] = kv.get('peak_detect', '0') in ('1', 'true')
         elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
             continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)
         elif name == 'eq':

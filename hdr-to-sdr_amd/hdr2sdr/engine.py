@@ -134,6 +134,18 @@ class Tonemapper:
                                             _abi.LOC_HOST, self._stream_ptr(None)))
         return out
 
+    # ---- dynamic peak (BT.2390 peak_detect) ----------------------------------
+    def reset_peak(self) -> None:
+        """Start a new sequence: forget the smoothed peak state."""
+        self._check(self._L.h2s_peak_reset(self._ctx))
+
+    def peak_state(self) -> 'dict[str, float]':
+        mx, avg, pk = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        self._check(self._L.h2s_peak_state(self._ctx, ctypes.byref(mx), ctypes.byref(avg), ctypes.byref(pk),
+                                           ctypes.byref(n)))
+        return {'max_pq': mx.value, 'avg_pq': avg.value, 'peak': pk.value, 'frames': n.value}
+
     # ---- timing (bench) -----------------------------------------------------
     def set_timing(self, enabled: bool) -> None:
         self._check(self._L.h2s_set_timing(self._ctx, 1 if enabled else 0))

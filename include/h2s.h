@@ -114,7 +114,10 @@ typedef struct h2s_params {
   int32_t lut_enabled;  /* 1: lut3d stage; 0: closed-form BT.2020->709     */
   int32_t mode;         /* enum h2s_mode                                   */
   int32_t desat_luma;   /* enum h2s_desat_luma                             */
-  int32_t reserved[5];
+  int32_t peak_detect;  /* BT.2390 only: 1 = per-frame detected, temporally
+                         * smoothed source peak (libplacebo peak_detect=1,
+                         * src/utils.py:448); state lives in the context   */
+  int32_t reserved[4];
 } h2s_params;
 
 /* A batch of planar 4:2:0 frames (yuv420p / yuv420p10le / yuv420p12le).
@@ -171,6 +174,14 @@ int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
  * device per out_location).  Synchronous. */
 int h2s_debug_float(h2s_ctx *ctx, const h2s_frames *in, int stage,
                     float *out_rgb, int out_location, void *hip_stream);
+
+/* ---- dynamic peak (params.peak_detect, BT.2390) --------------------------
+ * h2s_peak_reset: forget the smoothing state (a new sequence / scene cut).
+ * h2s_peak_state: the smoothed PQ-domain max / average after the last
+ *   processed frame, the source peak (units of npl) it gave, and the number
+ *   of frames folded in since the reset.  Any pointer may be NULL. */
+int h2s_peak_reset(h2s_ctx *ctx);
+int h2s_peak_state(const h2s_ctx *ctx, double *max_pq, double *avg_pq, double *peak, int64_t *frames);
 
 /* ---- preview (src/utils.py:719-765 extract_frame_with_conversion, the
  * GUI's adjust_gamma src/preview.py:108-117) ------------------------------

@@ -43,7 +43,8 @@ class Params(ctypes.Structure):
         ('gamma', ctypes.c_double), ('maxcll', ctypes.c_double),
         ('mastering_max', ctypes.c_double), ('lut_enabled', ctypes.c_int32),
         ('mode', ctypes.c_int32), ('desat_luma', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 5),
+        ('peak_detect', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 4),
     ]
 
 
@@ -102,6 +103,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_pq_eotf.argtypes = [ctypes.c_float]
         L.oracle_hlg_inverse_oetf.restype = ctypes.c_float
         L.oracle_hlg_inverse_oetf.argtypes = [ctypes.c_float]
+        L.oracle_peak_stats.restype = ctypes.c_int
+        L.oracle_peak_stats.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frames), ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_preview_tail.restype = ctypes.c_int
         L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
@@ -172,6 +176,65 @@ def preview_rgb24(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray,
     if rc:
         raise ValueError(f'oracle_preview_tail failed: {rc}')
     return out
+
+
+def peak_stats(params: Params, buf: np.ndarray, width: int, height: int) -> 'tuple[np.ndarray, np.ndarray]':
+    """Per-frame (max, mean) of the PQ-encoded max(R,G,B) (PARITY UNPINNED)."""
+    n = buf.shape[0]
+    fmax, favg = np.zeros(n), np.zeros(n)
+    d = _frames(np.ascontiguousarray(buf), width, height, params.bits_in)
+    rc = lib().oracle_peak_stats(ctypes.byref(params), ctypes.byref(d), n, fmax.ctypes.data, favg.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_peak_stats failed: {rc}')
+    return fmax, favg
+
+
+def pq_eotf_d(e: float) -> float:
+    """ST 2084 EOTF in double, 1.0 = 10000 nits."""
+    m1, m2 = 2610 / 16384, 2523 / 4096 * 128
+    c1, c2, c3 = 3424 / 4096, 2413 / 4096 * 32, 2392 / 4096 * 32
+    if not e > 0:
+        return 0.0
+    xp = e ** (1 / m2)
+    return (max(xp - c1, 0.0) / (c2 - c3 * xp)) ** (1 / m1)
+
+
+class PeakState:
+    """Restatement of the dynamic-peak smoothing (h2s_api.hip peak_update):
+    IIR with time constant 20 frames on the PQ max / average, bypassed by a
+    smoothstep over 10..30 % PQ average change; peak clamped to [1, static]."""
+
+    def __init__(self):
+        self.frames, self.max, self.avg = 0, 0.0, 0.0
+
+    def update(self, fmax: float, favg: float, static_peak: float) -> float:
+        if self.frames == 0:
+            self.max, self.avg = fmax, favg
+        else:
+            a = 1.0 - math.exp(-1.0 / 20.0)
+            t = min(max((abs(favg - self.avg) * 100.0 - 10.0) / 20.0, 0.0), 1.0)
+            w = a + (1.0 - a) * t * t * (3.0 - 2.0 * t)
+            self.max += w * (fmax - self.max)
+            self.avg += w * (favg - self.avg)
+        self.frames += 1
+        return min(max(pq_eotf_d(self.max) * 100.0, 1.0), static_peak)
+
+
+def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
+                    state: 'PeakState | None' = None) -> 'tuple[np.ndarray, list[float]]':
+    """BT.2390 with the detected peak: stats, smoothing, then each frame
+    through the chain with its own peak.  Returns (frames, peaks)."""
+    state = state or PeakState()
+    static_peak = resolved(params)[0]
+    fmax, favg = peak_stats(params, buf, width, height)
+    outs, peaks = [], []
+    for f in range(buf.shape[0]):
+        pk = state.update(float(fmax[f]), float(favg[f]), static_peak)
+        q = params_from(params)
+        q.peak = pk
+        outs.append(process(q, lattice, np.ascontiguousarray(buf[f:f + 1]), width, height))
+        peaks.append(pk)
+    return np.concatenate(outs), peaks
 
 
 def resolved(params: Params) -> 'tuple[float, float, np.ndarray]':

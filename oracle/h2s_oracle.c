@@ -658,3 +658,44 @@ int oracle_preview_tail(const uint8_t *yuv8, int W, int H, int ow, int oh, doubl
   free(tmp);
   return 0;
 }
+
+/* ---- dynamic peak statistics (params.peak_detect, BT.2390) ---------------
+ * PARITY UNPINNED (libplacebo absent): per frame, max and mean of the
+ * PQ-encoded max(R,G,B) over every pixel, nearest chroma; the smoothing is
+ * restated in oracle/__init__.py (PeakState). */
+int oracle_peak_stats(const h2s_params *p, const h2s_frames *in, int nframes, double *fmax, double *favg) {
+  const int sh = p->bits_in - 8;
+  const double ys = 1.0 / (219 << sh), yo = -(double)(16 << sh) / (219 << sh);
+  const double cs = 1.0 / (224 << sh), co = -(double)(128 << sh) / (224 << sh);
+  const double kr = 0.2627, kb = 0.0593, kg = 1.0 - kr - kb;
+  const double mrcr = 2 * (1 - kr), mgcb = -2 * kb * (1 - kb) / kg, mgcr = -2 * kr * (1 - kr) / kg, mbcb = 2 * (1 - kb);
+  const int W = in->width, H = in->height;
+  for (int f = 0; f < nframes; f++) {
+    double mx = 0, sm = 0;
+    for (int y = 0; y < H; y++)
+      for (int x = 0; x < W; x++) {
+        const double Y = rd(in, 0, f, x, y) * ys + yo;
+        const double cb = rd(in, 1, f, x / 2, y / 2) * cs + co, cr = rd(in, 2, f, x / 2, y / 2) * cs + co;
+        const double er = Y + mrcr * cr, eg = Y + mgcb * cb + mgcr * cr, eb = Y + mbcb * cb;
+        double m;
+        if (p->transfer_in == H2S_TRC_HLG) {
+          const double r = arib_b67_inverse_oetf((float)er), g = arib_b67_inverse_oetf((float)eg),
+                       b = arib_b67_inverse_oetf((float)eb);
+          const double l = 0.2627 * r + 0.6780 * g + 0.0593 * b;
+          const double w = l > 0 ? 1000.0 / p->npl * pow(l, 0.2) : 0.0;
+          double mm = r > g ? r : g;
+          mm = mm > b ? mm : b;
+          m = pq_encode_d(mm * w * p->npl / 10000.0);
+        } else {
+          m = er > eg ? er : eg;
+          m = m > eb ? m : eb;
+        }
+        m = m < 0 ? 0 : (m > 1 ? 1 : m);
+        mx = m > mx ? m : mx;
+        sm += m;
+      }
+    fmax[f] = mx;
+    favg[f] = sm / ((double)W * H);
+  }
+  return 0;
+}

@@ -1,0 +1,111 @@
+"""Dynamic peak for BT.2390 (libplacebo peak_detect=1, src/utils.py:448).
+
+PARITY UNPINNED against libplacebo (not in this image).  The model is stated
+in DESIGN.md and restated in the oracle: per-frame max / mean of the
+PQ-encoded max(R,G,B), an IIR with a 20-frame time constant that a
+smoothstep over a 10..30 % PQ change of the average bypasses at scene cuts,
+and the result clamped to [1, static peak].  The GPU path (per-frame stats
+kernel + host smoothing + per-frame BT.2390 constants) must match that
+restatement frame by frame, across calls on one context."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+import hdr2sdr
+from hdr2sdr.synth import synth_frames
+
+
+def test_peak_state_first_frame_constant_and_scene_cut():
+    st = oracle.PeakState()
+    p0 = st.update(0.6, 0.3, 40.0)
+    assert p0 == pytest.approx(oracle.pq_eotf_d(0.6) * 100)
+    for _ in range(5):                               # constant input: constant peak
+        assert st.update(0.6, 0.3, 40.0) == pytest.approx(p0)
+    st.update(0.7, 0.35, 40.0)                       # 5 % PQ change: plain IIR step
+    assert st.max == pytest.approx(0.6 + (1 - math.exp(-1 / 20)) * 0.1)
+    st.update(0.9, 0.8, 40.0)                        # ~45 % PQ change of the average: scene cut, jump
+    assert st.max == pytest.approx(0.9) and st.avg == pytest.approx(0.8)
+
+
+def test_peak_clamps_to_one_and_static_peak():
+    st = oracle.PeakState()
+    assert st.update(0.1, 0.05, 10.0) == 1.0         # below 100 nits -> 1
+    st = oracle.PeakState()
+    assert st.update(0.95, 0.5, 10.0) == 10.0        # above the static peak -> static
+
+
+def _flat_frame(code_y, code_c=512, W=64, H=32):
+    fb = hdr2sdr.FrameBatch.empty_numpy(1, W, H, 10)
+    fb.y[...] = code_y
+    fb.u[...] = code_c
+    fb.v[...] = code_c
+    return fb
+
+
+def test_oracle_peak_stats_neutral_frame():
+    code = 64 + round(0.5 * 876)                     # E = 0.5 on every channel
+    p = oracle.params_from(hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True).to_c())
+    mx, avg = oracle.peak_stats(p, _flat_frame(code).buf, 64, 32)
+    assert mx[0] == pytest.approx((code - 64) / 876, abs=1e-9) and avg[0] == pytest.approx(mx[0])
+
+
+def test_libplacebo_chain_turns_peak_detect_on():
+    params, _ = hdr2sdr.parse_filter_chain(
+        'format=p010,hwupload,libplacebo=w=iw:h=ih:tonemapping=bt.2390:colorspace=bt709:peak_detect=1:format=rgba,'
+        'hwdownload,format=rgba,lut3d=file=<LUT>:interp=tetrahedral')
+    assert params.peak_detect and params.tonemapper == 'bt.2390'
+
+
+def sequence(W=256, H=128):
+    """6 frames of different brightness with a scene cut at frame 3."""
+    frames = []
+    for i, k in enumerate((0.62, 0.62, 0.66, 0.30, 0.30, 0.64)):
+        f = synth_frames('smooth', 1, W, H, 10, device='cpu', seed=40 + i).to_numpy()
+        f.y[...] = (64 + (f.y.astype(np.float64) - 64) * k).round().astype(np.uint16)
+        f.u[...] = (512 + (f.u.astype(np.float64) - 512) * k).round().astype(np.uint16)
+        f.v[...] = (512 + (f.v.astype(np.float64) - 512) * k).round().astype(np.uint16)
+        frames.append(f.buf)
+    return np.concatenate(frames)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])     # fast path and generic kernel
+def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H):
+    from test_gpu_parity import assert_close_int, lattice
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    got = []
+    for a, b in ((0, 2), (2, 5), (5, 6)):            # the state carries across calls
+        src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf[a:b]), W, H, 10)
+        dst = hdr2sdr.FrameBatch.empty_numpy(b - a, W, H, 10)
+        tm.process(src, dst)
+        got.append(dst.buf)
+    state = tm.peak_state()
+    tm.close()
+    got = np.concatenate(got).astype(np.int64)
+    want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert len(set(round(p, 3) for p in peaks)) >= 3          # the peak really moves
+    assert state['frames'] == 6 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
+    assert_close_int(params, got, want.astype(np.int64), W, H)
+
+
+@pytest.mark.gpu
+def test_gpu_peak_reset_restarts_the_sequence():
+    from test_gpu_parity import lattice
+    buf = sequence()
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    one = hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:4]), 256, 128, 10)
+    out_a = hdr2sdr.FrameBatch.empty_numpy(1, 256, 128, 10)
+    tm.process(one, out_a)                             # first frame of a sequence
+    tm.process(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[:3]), 256, 128, 10),
+               hdr2sdr.FrameBatch.empty_numpy(3, 256, 128, 10))
+    tm.reset_peak()
+    out_b = hdr2sdr.FrameBatch.empty_numpy(1, 256, 128, 10)
+    tm.process(one, out_b)
+    assert tm.peak_state()['frames'] == 1
+    assert np.array_equal(out_a.buf, out_b.buf)
+    tm.close()
