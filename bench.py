@@ -163,6 +163,38 @@ def main():
         el_u, kms_u, px_u, _ = run('uniform')
         alt = {'kind': 'uniform', 'value': round(px_u / el_u / 1e6, 1), 'kernel_ms': round(kms_u, 4)}
 
+    # the other BASELINE.json configurations, single-GPU, for reference
+    # (not the headline value): kernel time on device-resident frames
+    other = None
+    if world == 1 and not args.no_alt:
+        other = {}
+        for tag, kw, w_, h_, nf, lut_n in (
+                ('C1', dict(tonemapper='reinhard', gamma=1.0, bits_out=8), 1920, 1080, 16, 33),
+                ('C3', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
+                ('C4', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
+                ('C5', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
+                 7680, 4320, 4, 65)):
+            p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
+            t_ = hdr2sdr.Tonemapper(local, p_, hdr2sdr.generate_lattice(lut_n))
+            src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)
+            dst_ = hdr2sdr.FrameBatch.empty_torch(nf, w_, h_, p_.bits_out, dev)
+            st_ = torch.cuda.current_stream(dev)
+            for _ in range(2):
+                t_.process(src_, dst_, st_)
+            torch.cuda.synchronize(dev)
+            t_.set_timing(True)
+            for _ in range(5):
+                t_.process(src_, dst_, st_)
+            torch.cuda.synchronize(dev)
+            kms_ = t_.kernel_ms(5)
+            b_ = 1.5 * (1 if p_.bits_in == 8 else 2) + 1.5 * (1 if p_.bits_out == 8 else 2)
+            other[tag] = {'size': f'{w_}x{h_}', 'frames': nf, 'tonemapper': kw['tonemapper'], 'lut': lut_n,
+                          'bits': f"{p_.bits_in}->{p_.bits_out}", 'kernel_ms': round(kms_, 4),
+                          'mpx_s': round(nf * w_ * h_ / kms_ / 1e3, 1),
+                          'hbm_frac': round(b_ * nf * w_ * h_ / (kms_ / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            t_.close()
+            del src_, dst_
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -195,6 +227,7 @@ def main():
             'content': args.kind,
             'parallelism': f'frame-sharded x{world} (RCCL LUT broadcast only)',
             'alt_content': alt,
+            'other_configs': other,
         },
         'roofline': {
             'bound': 'hbm',
