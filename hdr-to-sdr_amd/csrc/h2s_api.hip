@@ -605,6 +605,11 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
     F.out[p] = k.out[p], F.out_ls[p] = k.out_ls[p], F.out_fp[p] = k.out_fp[p];
   }
   F.W = k.W, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
+  for (int p = 0; p < 3; p++) {
+    const long long ib = (long long)(p ? k.ch : k.H) * k.in_ls[p], ob = (long long)(p ? k.ch : k.H) * k.out_ls[p];
+    F.in_bytes[p] = (int)(ib < 0x7fffffff ? ib : 0x7fffffff);
+    F.out_bytes[p] = (int)(ob < 0x7fffffff ? ob : 0x7fffffff);
+  }
   F.nbx = (unsigned)(k.W / 64);
   F.nby = (unsigned)((k.H + 31) / 32);
   F.nframes = (unsigned)nframes;

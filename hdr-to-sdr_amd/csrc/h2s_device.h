@@ -64,6 +64,7 @@ struct FastParams {
   long long in_ls[3], in_fp[3];
   uint8_t* out[3];
   long long out_ls[3], out_fp[3];
+  int in_bytes[3], out_bytes[3];   // plane extents for buffer resources (clamped to 2^31-1)
   // S1: R'G'B' = k + ys*Y + a*{U,V}; index [0] even columns (x4), [1] odd (x8)
   float ys, k_r, k_g, k_b;
   float a_rv[2], a_gv[2], a_gu[2], a_bu[2];

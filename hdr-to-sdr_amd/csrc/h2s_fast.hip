@@ -186,8 +186,9 @@ __device__ __forceinline__ T in_vgpr(T x) {
   return y;
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base, long long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+// bytes: the plane's extent, clamped to 2^31-1 on the host (FastParams in/out_bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
 }
 
 // one tile's global loads, held in registers between issue and the LDS commit
@@ -209,13 +210,23 @@ __device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) 
   return g;
 }
 
+// the tile after g in walk order (x, then y, then frame): block-uniform
+// scalar arithmetic, no division
+__device__ __forceinline__ void tile_next(const FastParams& F, TileGeo& g) {
+  g.px0 += TBW, g.cx0 += CBW;
+  if (g.px0 >= F.W) {
+    g.px0 = 0, g.cx0 = 0, g.py0 += TBH, g.cy0 += CBH;
+    if (g.py0 >= (int)F.nby * TBH) g.py0 = 0, g.cy0 = 0, g.f++;
+  }
+}
+
 // issue (do not wait for) the loads of one tile: luma 64 x 32 (one 16-byte
 // load per thread) and chroma rows cy0-1 .. cy0+16 (18 rows x 4 chunks of 8
 // samples + 1 right-halo sample; threads 0..71).  One thread loads the same
 // chunk of both planes, so each buffer resource stays wave-uniform (a per-lane
 // choice of resource becomes a waterfall loop).
 __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t) {
-  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], (long long)F.H * F.in_ls[0]);
+  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], F.in_bytes[0]);
   const int yr = t >> 3, yc = t & 7;
   TileRegs r;
   r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -223,8 +234,8 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
   r.ua = r.va = make_uint4(0, 0, 0, 0);
   r.uh = r.vh = 0;
   if (t < 72) {
-    const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], (long long)F.ch * F.in_ls[1]);
-    const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], (long long)F.ch * F.in_ls[2]);
+    const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], F.in_bytes[1]);
+    const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], F.in_bytes[2]);
     const int clr = t >> 2, ccx = t & 3;
     const int row = fedge(g.cy0 - 1 + clr, F.ch), hx = 2 * fedge(g.cx0 + 8 * ccx + 8, F.cw);
     const int ou = row * (int)F.in_ls[1], ov = row * (int)F.in_ls[2];
@@ -287,15 +298,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const int hb = pyl ? HST : -HST;
   float* csb = csum[0] + qy * CBW + 8 * w + qx;
 
+  // hot constants live in VGPRs for the whole kernel
+  const float k_r = in_vgpr(F.k_r) * (float)ESC, k_g = in_vgpr(F.k_g) * (float)ESC, k_b = in_vgpr(F.k_b) * (float)ESC;
+  const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
+              a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
+  const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
+  const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
+  const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
+  const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
+
   for (;;) {
     // ---- commit this tile's registers to LDS ----
     {
       float v[8];
       unpack8(cur.ya, v);
       float* d = yin + (t >> 3) * YST + 8 * (t & 7);
-      const float ys = F.ys * (float)ESC;   // zimg depth-conversion scale
-      *reinterpret_cast<float4*>(d) = make_float4(v[0] * ys, v[1] * ys, v[2] * ys, v[3] * ys);
-      *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ys, v[5] * ys, v[6] * ys, v[7] * ys);
+      *reinterpret_cast<float4*>(d) = make_float4(v[0] * ysc, v[1] * ysc, v[2] * ysc, v[3] * ysc);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ysc, v[5] * ysc, v[6] * ysc, v[7] * ysc);
     }
     if (t < 72) {
       // horizontal pass (left siting, x2 scale): h[2k] = 2 c[k],
@@ -316,18 +335,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
-      geo = tile_geo(F, tile + 1);
+      tile_next(F, geo);
       cur = tile_load(F, geo, t);        // in flight during this tile's compute
     }
     __syncthreads();
 
-    // hot constants live in VGPRs
-    const float k_r = in_vgpr(F.k_r) * (float)ESC, k_g = in_vgpr(F.k_g) * (float)ESC, k_b = in_vgpr(F.k_b) * (float)ESC;
-    const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
-                a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
-    const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
-    const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
-    const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
     const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
@@ -373,7 +385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
     // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
     {
-      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], (long long)F.H * F.out_ls[0]);
+      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
       const int r = t >> 3, c = t & 7;
       if (g.py0 + r < F.H) {
         const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
@@ -399,7 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         unsigned code[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
-        const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], (long long)F.ch * F.out_ls[1 + pl]);
+        const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
         const int off = (g.cy0 + r) * (int)F.out_ls[1 + pl];
         if (F.out8)
           __builtin_amdgcn_raw_buffer_store_b64(
