@@ -17,7 +17,7 @@ namespace h2s {
 hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
 hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
 bool fast_supported(int tonemap);
-hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStream_t s);
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
                             long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
@@ -614,7 +614,8 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.nby = (unsigned)((k.H + 31) / 32);
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
-  return h2s::launch_fast(F, k.transfer, k.tonemap, k.desat_on != 0, s);
+  const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
+  return h2s::launch_fast(F, k.transfer, k.tonemap, desat, s);
 }
 
 // libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):

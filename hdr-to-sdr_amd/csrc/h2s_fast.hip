@@ -78,8 +78,11 @@ __device__ __forceinline__ float pq_table(const float4* tab, float e) {
 }
 
 // S1 transfer to linear (units of npl), specialised
+// returns true (wave-uniform) when some lane of the wave took the exact PQ
+// path: linear values may then be huge or infinite, and the tone curve must
+// use its overflow-safe form
 template <int TRC, int ESC = 1>
-__device__ __forceinline__ void to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
+__device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
                                           float& r, float& g, float& b) {
   if (TRC == 0) {
     r = pq_table<ESC>(pq_lds, er), g = pq_table<ESC>(pq_lds, eg), b = pq_table<ESC>(pq_lds, eb);
@@ -89,7 +92,9 @@ __device__ __forceinline__ void to_linear(const FastParams& F, const float4* pq_
       r = er >= EL ? pq_exact(F, er * EI) : r;
       g = eg >= EL ? pq_exact(F, eg * EI) : g;
       b = eb >= EL ? pq_exact(F, eb * EI) : b;
+      return true;
     }
+    return false;
   } else {
     // zimg arib_b67_inverse_oetf, branch-free; then the OOTF (gamma 1.2)
     auto inv = [](float e) -> float {
@@ -102,12 +107,22 @@ __device__ __forceinline__ void to_linear(const FastParams& F, const float4* pq_
     const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
     const float w = fexp2(flog2(ys) * 0.2f + F.log2_lin_scale);  // ys == 0 -> 0
     r *= w, g *= w, b *= w;
+    return false;  // HLG is bounded (E <= 2.2 -> a few 1e4)
   }
 }
 
-// S2 vf_tonemap, specialised; returns the gain k = sig'/sig applied to rgb
-template <int TM, bool DESAT>
-__device__ __forceinline__ void tone(const FastParams& F, float& r, float& g, float& b) {
+// S2 vf_tonemap, specialised.  DESAT: 0 off, 1 weighted luma (F.lr/lg/lb),
+// 2 the RGB-coefficient luma r+g+b (vf_tonemap's table entry for the linear
+// RGB frame zscale hands it; the default).
+//
+// Bounded form (every lane's linear values from the PQ table or HLG, so
+// sig <= ~6e8 and den*sig cannot overflow): the desaturation and the gain
+// fold into out = c*A + B with A = (1-ob)*k, B = L*ob*k, since
+// max(c*(1-ob) + L*ob) = max(c)*(1-ob) + L*ob for 0 <= ob <= 1; the curve
+// uses one reciprocal.  Safe form (the wave met the exact PQ path): the
+// statement order of vf_tonemap, two reciprocals.
+template <int TM, int DESAT>
+__device__ __forceinline__ void tone(const FastParams& F, float& r, float& g, float& b, bool safe) {
   if (TM == 7) {  // BT.2390 (no desat), branch-free PQ encode / decode
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
     const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
@@ -126,29 +141,56 @@ __device__ __forceinline__ void tone(const FastParams& F, float& r, float& g, fl
     r *= k, g *= k, b *= k;
     return;
   }
-  if (DESAT) {
-    const float luma = F.lr * r + F.lg * g + F.lb * b;
-    const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
-    const float iob = 1.0f - ob;
-    r = r * iob + luma * ob;
-    g = g * iob + luma * ob;
-    b = b * iob + luma * ob;
+  if (safe) {
+    if (DESAT) {
+      const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
+      const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
+      const float iob = 1.0f - ob;
+      r = r * iob + luma * ob;
+      g = g * iob + luma * ob;
+      b = b * iob + luma * ob;
+    }
+    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
+    float k;
+    if (TM == 4) {  // REINHARD: sig/(sig+p) * (peak+p)/peak
+      k = F.rein_k * frcp(sig + F.rein_p);
+    } else if (TM == 5) {  // HABLE: hable(sig) / hable(peak)
+      const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
+      const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
+      k = fmaf(num * frcp(den), F.hable_peak_inv, -F.hable_ef_peak_inv) * frcp(sig);
+    } else {  // MOBIUS: identity below j
+      const float m = F.mob_k * (sig + F.mob_a) * frcp(sig + F.mob_b) * frcp(sig);
+      k = sig <= F.mob_j ? 1.0f : m;
+    }
+    r *= k, g *= k, b *= k;
+    return;
   }
-  const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-  // gain k = curve(sig) / sig with one reciprocal
+  float sig, A = 1.0f, B = 0.0f;
+  if (DESAT) {
+    const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
+    const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
+    A = 1.0f - ob, B = luma * ob;
+    sig = fmaxf(fmaf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), A, B), 1e-6f);
+  } else {
+    sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
+  }
   float k;
-  if (TM == 4) {  // REINHARD: sig/(sig+p) * (peak+p)/peak
+  if (TM == 4) {
     k = F.rein_k * frcp(sig + F.rein_p);
-  } else if (TM == 5) {  // HABLE: hable(sig) / hable(peak); two reciprocals keep
-    // huge (out-of-range) sig from overflowing den * sig
+  } else if (TM == 5) {  // (num hpi - ef hpi den) / (den sig): one reciprocal
     const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
     const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
-    k = fmaf(num * frcp(den), F.hable_peak_inv, -F.hable_ef_peak_inv) * frcp(sig);
-  } else {  // MOBIUS: identity below j
-    const float m = F.mob_k * (sig + F.mob_a) * frcp(sig + F.mob_b) * frcp(sig);
+    k = fmaf(num, F.hable_peak_inv, -F.hable_ef_peak_inv * den) * frcp(den * sig);
+  } else {
+    const float m = F.mob_k * (sig + F.mob_a) * frcp((sig + F.mob_b) * sig);
     k = sig <= F.mob_j ? 1.0f : m;
   }
-  r *= k, g *= k, b *= k;
+  if (DESAT) {
+    A *= k, B *= k;
+    r = fmaf(r, A, B), g = fmaf(g, A, B), b = fmaf(b, A, B);
+  } else {
+    r *= k, g *= k, b *= k;
+  }
 }
 
 // S3 + S4 coordinates: s = clamp((N-1) * x^(1/2.4)), as lattice units
@@ -252,7 +294,7 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 // are issued before tile i is computed, so after the first tile the block no
 // longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
 // barrier, 8 compute steps, barrier, store, barrier.
-template <int TRC, int TM, bool DESAT>
+template <int TRC, int TM, int DESAT>
 // 5 waves per SIMD = the LDS-bound occupancy (5 blocks of ~27.6 KB per CU;
 // 3 and 6 measured slower): let the compiler use the VGPRs that allows
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
@@ -299,7 +341,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   float* csb = csum[0] + qy * CBW + 8 * w + qx;
 
   // hot constants live in VGPRs for the whole kernel
-  const float k_r = in_vgpr(F.k_r) * (float)ESC, k_g = in_vgpr(F.k_g) * (float)ESC, k_b = in_vgpr(F.k_b) * (float)ESC;
+  const float k_r = in_vgpr(F.k_r) * (float)ESC;
+  const float dk_g = (in_vgpr(F.k_g) - in_vgpr(F.k_r)) * (float)ESC, dk_b = (in_vgpr(F.k_b) - in_vgpr(F.k_r)) * (float)ESC;
   const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
               a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
   const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
@@ -313,8 +356,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       float v[8];
       unpack8(cur.ya, v);
       float* d = yin + (t >> 3) * YST + 8 * (t & 7);
-      *reinterpret_cast<float4*>(d) = make_float4(v[0] * ysc, v[1] * ysc, v[2] * ysc, v[3] * ysc);
-      *reinterpret_cast<float4*>(d + 4) = make_float4(v[4] * ysc, v[5] * ysc, v[6] * ysc, v[7] * ysc);
+      // staged luma carries the red offset: Y*ys + k_r
+      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, k_r), fmaf(v[1], ysc, k_r), fmaf(v[2], ysc, k_r), fmaf(v[3], ysc, k_r));
+      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, k_r), fmaf(v[5], ysc, k_r), fmaf(v[6], ysc, k_r), fmaf(v[7], ysc, k_r));
     }
     if (t < 72) {
       // horizontal pass (left siting, x2 scale): h[2k] = 2 c[k],
@@ -349,12 +393,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const float ybs = ybase[oy];
       const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
       const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
-      const float er = fmaf(V, a_rv, ybs + k_r);
-      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + k_g));
-      const float eb = fmaf(U, a_bu, ybs + k_b);
+      const float er = fmaf(V, a_rv, ybs);
+      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + dk_g));
+      const float eb = fmaf(U, a_bu, ybs + dk_b);
       float r, gg, bl;
-      to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
-      tone<TM, DESAT>(F, r, gg, bl);
+      const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
+      tone<TM, DESAT>(F, r, gg, bl, safe);
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
       const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
@@ -449,30 +493,37 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 }
 
 #define FAST_CASES(X) \
-  X(0, 4, false)      \
-  X(0, 4, true)       \
-  X(0, 5, false)      \
-  X(0, 5, true)       \
-  X(0, 6, false)      \
-  X(0, 6, true)       \
-  X(0, 7, false)      \
-  X(1, 4, false)      \
-  X(1, 4, true)       \
-  X(1, 5, false)      \
-  X(1, 5, true)       \
-  X(1, 6, false)      \
-  X(1, 6, true)       \
-  X(1, 7, false)
+  X(0, 4, 0)          \
+  X(0, 4, 1)          \
+  X(0, 4, 2)          \
+  X(0, 5, 0)          \
+  X(0, 5, 1)          \
+  X(0, 5, 2)          \
+  X(0, 6, 0)          \
+  X(0, 6, 1)          \
+  X(0, 6, 2)          \
+  X(0, 7, 0)          \
+  X(1, 4, 0)          \
+  X(1, 4, 1)          \
+  X(1, 4, 2)          \
+  X(1, 5, 0)          \
+  X(1, 5, 1)          \
+  X(1, 5, 2)          \
+  X(1, 6, 0)          \
+  X(1, 6, 1)          \
+  X(1, 6, 2)          \
+  X(1, 7, 0)
 
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 7; }
 
-hipError_t launch_fast(const FastParams& F, int trc, int tm, bool desat, hipStream_t s) {
+// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
   if (nt == 0) return hipSuccess;
   const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb), block(256);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
-  if (tm == 7) desat = false;
+  if (tm == 7) desat = 0;
 #define K_FAST k_tile
 #define X(T, M, D)                                                   \
   if (trc == T && tm == M && desat == D) {                           \
