@@ -163,6 +163,25 @@ def main():
         el_u, kms_u, px_u, _ = run('uniform')
         alt = {'kind': 'uniform', 'value': round(px_u / el_u / 1e6, 1), 'kernel_ms': round(kms_u, 4)}
 
+    # PCIe-inclusive rate (host-resident, page-locked frames through the
+    # h2s_process host path: H2D, kernel, D2H): what the drop-in planner's
+    # pipes see.  Reported beside, never as, the headline value.
+    host_path = None
+    if world == 1 and not args.no_alt:
+        hs = synth_frames(args.kind, B, W, H, args.bits_in, device='cpu', seed=0x5EED).to_numpy()
+        hsrc = hdr2sdr.FrameBatch.empty_pinned(B, W, H, args.bits_in)
+        hsrc.buf[...] = hs.buf
+        hdst = hdr2sdr.FrameBatch.empty_pinned(B, W, H, args.bits_out)
+        tm.process(hsrc, hdst)
+        n_it, t0 = 5, time.perf_counter()
+        for _ in range(n_it):
+            tm.process(hsrc, hdst)
+        el_h = time.perf_counter() - t0
+        host_path = {'mpx_s': round(n_it * B * W * H / el_h / 1e6, 1), 'ms_per_step': round(el_h / n_it * 1e3, 3),
+                     'pinned': hsrc.buf.ctypes.data != 0 and hasattr(hsrc, '_pin'),
+                     'note': 'host frames in, host frames out; synchronous per call (no copy/compute overlap)'}
+        del hs, hsrc, hdst
+
     # the other BASELINE.json configurations, single-GPU, for reference
     # (not the headline value): kernel time on device-resident frames
     other = None
@@ -228,6 +247,7 @@ def main():
             'parallelism': f'frame-sharded x{world} (RCCL LUT broadcast only)',
             'alt_content': alt,
             'other_configs': other,
+            'host_path': host_path,
         },
         'roofline': {
             'bound': 'hbm',

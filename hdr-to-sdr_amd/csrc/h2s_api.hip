@@ -346,8 +346,20 @@ h2s_frames tight(const h2s_frames* f, void* base) {
   return t;
 }
 
+// the whole batch is one contiguous span laid out as tight() describes
+bool is_tight(const h2s_frames* f) {
+  const long long bps = f->bits == 8 ? 1 : 2;
+  const long long ysz = (long long)f->width * f->height * bps, csz = ysz / 4, fb = ysz + 2 * csz;
+  return f->linesize[0] == f->width * bps && f->linesize[1] == f->width / 2 * bps &&
+         f->linesize[2] == f->width / 2 * bps && f->frame_pitch[0] == fb && f->frame_pitch[1] == fb &&
+         f->frame_pitch[2] == fb && (const uint8_t*)f->data[1] == (const uint8_t*)f->data[0] + ysz &&
+         (const uint8_t*)f->data[2] == (const uint8_t*)f->data[1] + csz;
+}
+
 hipError_t copy_frames(const h2s_frames* dst, const h2s_frames* src, int nframes, hipStream_t s) {
   const long long bps = src->bits == 8 ? 1 : 2;
+  if (is_tight(src) && is_tight(dst))  // one DMA for the whole batch
+    return hipMemcpyAsync(dst->data[0], src->data[0], (size_t)src->frame_pitch[0] * nframes, hipMemcpyDefault, s);
   for (int fr = 0; fr < nframes; fr++)
     for (int p = 0; p < 3; p++) {
       const long long w = (p ? src->width / 2 : src->width) * bps, h = p ? src->height / 2 : src->height;

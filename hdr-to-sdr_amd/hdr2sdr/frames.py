@@ -65,6 +65,24 @@ class FrameBatch:
         return cls(np.zeros(cls._shape(nframes, width, height, bits), dtype=dt), width, height, bits)
 
     @classmethod
+    def empty_pinned(cls, nframes: int, width: int, height: int, bits: int) -> 'FrameBatch':
+        """Host batch in page-locked memory (DMA-able without a bounce copy:
+        the host-buffer path of h2s_process then runs at PCIe speed). Falls
+        back to pageable numpy memory when no GPU runtime is present."""
+        try:
+            import torch
+            if torch.cuda.is_available():
+                dt = torch.uint8 if bits == 8 else torch.int16
+                t = torch.empty(cls._shape(nframes, width, height, bits), dtype=dt, pin_memory=True)
+                a = t.numpy() if bits == 8 else t.numpy().view(np.uint16)
+                fb = cls(a, width, height, bits)
+                fb._pin = t          # keep the pinned allocation alive
+                return fb
+        except (ImportError, RuntimeError):
+            pass
+        return cls.empty_numpy(nframes, width, height, bits)
+
+    @classmethod
     def from_planes(cls, y: np.ndarray, u: np.ndarray, v: np.ndarray, bits: int) -> 'FrameBatch':
         """Pack [F,H,W] / [F,H/2,W/2] numpy planes into a batch."""
         f, h, w = y.shape

@@ -172,8 +172,9 @@ class H2SProcess:
         self.enc = popen(plan.encode, stdin=subprocess.PIPE, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL)
         self.stderr = io.TextIOWrapper(self.enc.stderr, encoding='utf-8', errors='replace')
         p = plan.params
-        self._src = FrameBatch.empty_numpy(self._batch, plan.width, plan.height, p.bits_in)
-        self._dst = FrameBatch.empty_numpy(self._batch, plan.width, plan.height, p.bits_out)
+        # page-locked staging: the pipe bytes go straight to / from HBM by DMA
+        self._src = FrameBatch.empty_pinned(self._batch, plan.width, plan.height, p.bits_in)
+        self._dst = FrameBatch.empty_pinned(self._batch, plan.width, plan.height, p.bits_out)
         self.frames = 0
         self._thread = threading.Thread(target=self._pump, name='h2s-pump', daemon=True)
         self._thread.start()
