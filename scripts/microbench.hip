@@ -69,6 +69,11 @@ UNARY_KERNEL(k_fmaak, "v_fmaak_f32 %0, %0, %0, 0x3e000000")
 UNARY_KERNEL(k_mulu24, "v_mul_u32_u24 %0, 7, %0")
 UNARY_KERNEL(k_mullo, "v_mul_lo_u32 %0, %0, %0")
 UNARY_KERNEL(k_lshladd, "v_lshl_add_u32 %0, %0, 2, %0")
+UNARY_KERNEL(k_cvtu, "v_cvt_u32_f32 %0, %0")
+UNARY_KERNEL(k_cvtflr, "v_cvt_flr_i32_f32 %0, %0")
+UNARY_KERNEL(k_bfe, "v_bfe_u32 %0, %0, 4, 8")
+UNARY_KERNEL(k_andor, "v_and_or_b32 %0, %0, -16, 5")
+UNARY_KERNEL(k_lshl16, "v_lshlrev_b16 %0, 1, %0")
 
 __global__ __launch_bounds__(256) void k_pkfma32(float* out, float seed) {
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -178,6 +183,8 @@ int main() {
       {"v_add_u32", k_addu, 8}, {"v_lshlrev_b32", k_lsh, 8}, {"v_and_b32", k_and, 8}, {"v_mov_b32", k_mov, 8},
       {"v_mov_b32_dpp", k_movdpp, 8}, {"v_add_f32_dpp", k_adddpp, 8}, {"v_floor_f32", k_floor, 8},
       {"v_mul_u32_u24", k_mulu24, 8}, {"v_mul_lo_u32", k_mullo, 8}, {"v_lshl_add_u32", k_lshladd, 8},
+      {"v_cvt_u32_f32", k_cvtu, 8}, {"v_cvt_flr_i32_f32", k_cvtflr, 8}, {"v_bfe_u32", k_bfe, 8},
+      {"v_and_or_b32", k_andor, 8}, {"v_lshlrev_b16", k_lshl16, 8},
   };
   const double waves = blocks * 4.0, cus = 256, clk = 2.4e9;
   double fma_rate = 0;
