@@ -7,7 +7,7 @@ Usage: python scripts/isa_cost.py file.s kernel_symbol"""
 import re
 import sys
 
-FULL = re.compile(r'v_(fma|fmac|fmaak|fmamk|mul|add|sub|subrev)_f32|v_(add|sub|subrev)_u32|v_(and|or|xor)_b32|v_mov_b32_e32|v_mov_b64')
+FULL = re.compile(r'v_(fma|fmac|fmaak|fmamk|mul|add|sub|subrev)_f32|v_(add|sub|subrev)_u32|v_(and|or|xor)_b32|v_mov_b32_e32|v_mov_b64|v_lshlrev_b16|v_(add|sub)_u16')
 TRANS = re.compile(r'v_(exp|log|rcp|rsq|sqrt|sin|cos)_f32')
 PK = re.compile(r'v_pk_(fma|mul|add)_f32')
 
