@@ -93,3 +93,25 @@ def test_null_handling_without_device():
         _abi.raise_for(_abi.H2S_E_LUT_MISSING, 'x')
     with pytest.raises(RuntimeError):
         _abi.raise_for(_abi.H2S_E_HIP, 'x')
+
+
+def test_product_path_fails_loudly_without_the_library(tmp_path):
+    """No CPU fallback: with libh2s missing, the first pixel call raises
+    ImportError (the package itself still imports)."""
+    import subprocess
+    import sys
+    code = ('import sys; sys.path.insert(0, %r); import hdr2sdr\n'
+            'try:\n    hdr2sdr.Tonemapper(0)\nexcept ImportError as e:\n    print("IMPORTERROR", e)\n'
+            'else:\n    print("NO ERROR")\n') % os.path.join(REPO, 'hdr-to-sdr_amd')
+    env = dict(os.environ, H2S_LIB=str(tmp_path / 'missing' / 'libh2s.so'))
+    out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=120)
+    assert 'IMPORTERROR' in out.stdout, out.stdout + out.stderr
+
+
+def test_host_package_never_imports_the_oracle():
+    """Only tests, smoke() and bench's cpu_baseline may touch oracle/."""
+    pkg = os.path.join(REPO, 'hdr-to-sdr_amd', 'hdr2sdr')
+    for name in os.listdir(pkg):
+        if name.endswith('.py'):
+            src = open(os.path.join(pkg, name)).read()
+            assert not re.search(r'^\s*(import|from)\s+oracle\b', src, flags=re.M), name
