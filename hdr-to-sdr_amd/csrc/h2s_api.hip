@@ -549,6 +549,7 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->b_srcmin = k.b_srcmin, F->b_range = k.b_range, F->b_inv_range = k.b_inv_range;
   F->b_ks = k.b_ks, F->b_inv_1mks = k.b_inv_1mks, F->b_maxlum = k.b_maxlum;
   F->npl_1e4 = k.npl_1e4, F->e4_npl = k.e4_npl;
+  F->b_e1min = (float)pq_encode_d(1e-6 * p->npl / 10000.0);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);

@@ -75,6 +75,7 @@ struct FastParams {
   float hable_peak_inv, hable_ef_peak_inv;
   float mob_j, mob_a, mob_b, mob_k;
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
+  float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 e1 lower bound)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)

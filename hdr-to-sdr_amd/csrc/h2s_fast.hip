@@ -121,22 +121,37 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // max(c*(1-ob) + L*ob) = max(c)*(1-ob) + L*ob for 0 <= ob <= 1; the curve
 // uses one reciprocal.  Safe form (the wave met the exact PQ path): the
 // statement order of vf_tonemap, two reciprocals.
-template <int TM, int DESAT>
-__device__ __forceinline__ void tone(const FastParams& F, float& r, float& g, float& b, bool safe) {
-  if (TM == 7) {  // BT.2390 (no desat), branch-free PQ encode / decode
+//
+// BT.2390 on PQ input (TRC 0, bounded form): the EETF's first step encodes
+// sig = max(R,G,B) back to PQ, and PQ(EOTF(max E)) = max E, so e1 is the
+// input's own max code value (emax_s = max E * PQ_SEG, clamped below at the
+// code of sig = 1e-6); the final decode reads the EOTF table already in LDS.
+template <int TRC, int TM, int DESAT>
+__device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, float& r, float& g, float& b,
+                                     bool safe, float emax_s) {
+  if (TM == 7) {  // BT.2390 (no desat)
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-    const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
-    const float e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
+    float e1;
+    if (TRC == 0 && !safe) {
+      e1 = fmaxf(emax_s * (1.0f / (float)PQ_SEG), F.b_e1min);
+    } else {  // exact PQ encode: HLG input, or the wave met the exact EOTF path
+      const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
+      e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
+    }
     const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
-    float e2 = e1n;
     const float t = (e1n - F.b_ks) * F.b_inv_1mks;
     const float t2 = t * t, t3 = t2 * t;
     const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
                     (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
-    e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
-    const float e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);
-    const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
-    const float s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
+    const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
+    const float e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
+    float s2;
+    if (TRC == 0) {
+      s2 = pq_table<PQ_SEG>(pq_lds, e4 * (float)PQ_SEG);          // EOTF(e4) * 10000/npl
+    } else {
+      const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
+      s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
+    }
     const float k = s2 * frcp(sig);
     r *= k, g *= k, b *= k;
     return;
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const float eb = fmaf(U, a_bu, ybs + dk_b);
       float r, gg, bl;
       const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
-      tone<TM, DESAT>(F, r, gg, bl, safe);
+      tone<TRC, TM, DESAT>(F, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
       const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
