@@ -56,6 +56,25 @@ def parse_cube(text: 'str | bytes') -> np.ndarray:
     return out
 
 
+def escape_path_for_filter(path: str) -> str:
+    """src/utils.py:188-204 _escape_path_for_filter: backslashes become '/',
+    and the first ':' (the drive colon) becomes two backslashes + ':', as
+    ffmpeg's filtergraph parser needs inside lut3d=file=..."""
+    return path.replace('\\', '/').replace(':', '\\\\:', 1)
+
+
+_LUT_FILTER_PATH: 'str | None' = None
+
+
+def get_lut_filter_path() -> str:
+    """src/utils.py:212-225 get_lut_filter_path: the bundled-equivalent
+    .cube's path, escaped for direct embedding in the chain string, cached."""
+    global _LUT_FILTER_PATH
+    if _LUT_FILTER_PATH is None:
+        _LUT_FILTER_PATH = escape_path_for_filter(lut_path())
+    return _LUT_FILTER_PATH
+
+
 def unescape_filter_path(path: str) -> str:
     """Inverse of the reference's _escape_path_for_filter (src/utils.py:188-204):
     the drive colon was written as two backslashes + ':' for the filtergraph."""

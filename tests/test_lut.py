@@ -94,3 +94,20 @@ def test_lut_path_generates_once(tmp_path, hashes):
     assert lut.lut_path(str(tmp_path), size=17) == p and os.path.getmtime(p) == m
     with pytest.raises(FileNotFoundError):
         lut.load_cube(str(tmp_path / 'missing.cube'))
+
+
+@pytest.mark.parametrize('raw,esc', [
+    (r'C:\Program Files\HDR\luts\rec2020_to_rec709.cube', r'C\\:/Program Files/HDR/luts/rec2020_to_rec709.cube'),
+    ('/opt/app/luts/rec2020_to_rec709.cube', '/opt/app/luts/rec2020_to_rec709.cube'),
+    (r'D:\a:b.cube', r'D\\:/a:b.cube'),      # only the first colon is escaped
+])
+def test_escape_path_for_filter_matches_reference_rule(raw, esc):
+    from hdr2sdr.lut import escape_path_for_filter, unescape_filter_path
+    assert escape_path_for_filter(raw) == esc
+    assert unescape_filter_path(esc) == raw.replace('\\', '/')
+
+
+def test_get_lut_filter_path_points_at_the_generated_cube():
+    from hdr2sdr.lut import get_lut_filter_path, unescape_filter_path, load_cube, generate_lattice
+    p = unescape_filter_path(get_lut_filter_path())
+    assert np.array_equal(load_cube(p), generate_lattice(65))
