@@ -214,3 +214,73 @@ def test_full_size_uniform_worst_case(tm):
     params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=10)
     got, want, _ = run_both(tm, params, 'uniform', 3840, 2160, nframes=1)
     assert_close_int(params, got, want, 3840, 2160)
+
+
+def _padded_descriptor(buf, W, H, bits, ls_pad, fp_pad):
+    """h2s_frames over a torch uint8 byte buffer with row padding and frame gaps."""
+    from hdr2sdr import _abi
+    sb = 1 if bits == 8 else 2
+    ls = [W * sb + ls_pad, W // 2 * sb + ls_pad // 2, W // 2 * sb + ls_pad // 2]
+    ysz, csz = H * ls[0], H // 2 * ls[1]
+    fp = ysz + 2 * csz + fp_pad
+    d = _abi.H2SFrames()
+    base = buf.data_ptr()
+    d.data[0], d.data[1], d.data[2] = base, base + ysz, base + ysz + csz
+    for p in range(3):
+        d.linesize[p], d.frame_pitch[p] = ls[p], fp
+    d.width, d.height, d.bits, d.location = W, H, bits, _abi.LOC_DEVICE
+    return d, ls, fp
+
+
+def _pack_padded(tight, W, H, bits, ls, fp):
+    """Copy a tight [F, W*H*3/2] batch into a padded byte layout (numpy)."""
+    sb = 1 if bits == 8 else 2
+    F = tight.shape[0]
+    raw = np.zeros((F * fp + 64,), dtype=np.uint8)
+    tb = tight.view(np.uint8).reshape(F, -1)
+    for f in range(F):
+        off_t, off_p = 0, f * fp
+        for p, (w, h) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            for r in range(h):
+                raw[off_p + r * ls[p]: off_p + r * ls[p] + w * sb] = tb[f, off_t + r * w * sb: off_t + (r + 1) * w * sb]
+            off_t += w * h * sb
+            off_p += h * ls[p]
+    return raw
+
+
+def _unpack_padded(raw, F, W, H, bits, ls, fp):
+    sb = 1 if bits == 8 else 2
+    out = np.zeros((F, W * H * 3 // 2 * sb), dtype=np.uint8)
+    for f in range(F):
+        off_t, off_p = 0, f * fp
+        for p, (w, h) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            for r in range(h):
+                out[f, off_t + r * w * sb: off_t + (r + 1) * w * sb] = raw[off_p + r * ls[p]: off_p + r * ls[p] + w * sb]
+            off_t += w * h * sb
+            off_p += h * ls[p]
+    return out.view(np.uint8 if bits == 8 else np.uint16)
+
+
+@pytest.mark.parametrize('bits_out', [10, 8])
+def test_padded_strides_and_frame_gaps(tm, bits_out):
+    """Row padding (linesize > width) and gaps between frames, on both sides,
+    through the tile kernel (16-byte aligned) — equal to the tight result."""
+    import ctypes
+    import torch
+    W, H, F = 256, 96, 3
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out)
+    got_tight, want, _ = run_both(tm, params, 'smooth', W, H, nframes=F)
+    src = synth_frames('smooth', F, W, H, 10, device='cpu', seed=11).to_numpy()
+    # input: 32 bytes of row padding, 4 KiB between frames
+    probe = torch.zeros(1, dtype=torch.uint8)
+    _, in_ls, in_fp = _padded_descriptor(probe, W, H, 10, 32, 4096)
+    raw_in = torch.from_numpy(_pack_padded(src.buf, W, H, 10, in_ls, in_fp)).cuda()
+    in_d, _, _ = _padded_descriptor(raw_in, W, H, 10, 32, 4096)
+    _, out_ls, out_fp = _padded_descriptor(probe, W, H, bits_out, 64, 512)
+    raw_out = torch.zeros(F * out_fp + 64, dtype=torch.uint8, device='cuda')
+    out_d, _, _ = _padded_descriptor(raw_out, W, H, bits_out, 64, 512)
+    tm._check(tm._L.h2s_process(tm._ctx, ctypes.byref(in_d), ctypes.byref(out_d), F, None))
+    torch.cuda.synchronize()
+    got = _unpack_padded(raw_out.cpu().numpy(), F, W, H, bits_out, out_ls, out_fp).astype(np.int64)
+    assert np.array_equal(got, got_tight)
+    assert_close_int(params, got, want, W, H)
