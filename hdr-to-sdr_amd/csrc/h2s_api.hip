@@ -34,6 +34,7 @@ using h2s::KParams;
 namespace {
 thread_local std::string g_err;  // errors with no context
 constexpr int kEvRing = 256;
+constexpr int kMaxChunks = 8;  // host-frame pipeline depth (chunks per call)
 }  // namespace
 
 struct h2s_ctx {
@@ -46,6 +47,7 @@ struct h2s_ctx {
   float* d_lut_yuv = nullptr;  // lattice pre-multiplied into output code space (3 floats/point)
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
   bool fast_enabled = true;
+  bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
@@ -62,6 +64,10 @@ struct h2s_ctx {
   bool timing = false;
   hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
   long long ev_count = 0;  // launches recorded since reset
+  // host-frame pipeline: H2D, compute and D2H of consecutive chunks on
+  // their own streams (two DMA directions overlap the kernel and each other)
+  hipStream_t ps[3] = {};
+  hipEvent_t pev[2 * kMaxChunks + 2] = {};
 };
 
 namespace {
@@ -430,6 +436,7 @@ int h2s_create(int device, h2s_ctx** out) {
   if (!c) return fail(nullptr, H2S_E_OOM, "context allocation failed");
   c->device = device;
   h2s_params_default(&c->params);
+  if (const char* v = getenv("H2S_HOST_SERIAL")) c->serial_host = atoi(v) != 0;
   if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
     const int tpb = atoi(v);
     if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
@@ -453,6 +460,10 @@ void h2s_destroy(h2s_ctx* c) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
   }
+  for (hipEvent_t ev : c->pev)
+    if (ev) hipEventDestroy(ev);
+  for (hipStream_t ps : c->ps)
+    if (ps) hipStreamDestroy(ps);
   delete c;
 }
 
@@ -710,6 +721,93 @@ int h2s_peak_state(const h2s_ctx* c, double* max_pq, double* avg_pq, double* pea
   return 0;
 }
 
+// frames [start, ...) of a batch
+static h2s_frames frames_at(const h2s_frames* f, int start) {
+  h2s_frames t = *f;
+  for (int p = 0; p < 3; p++) t.data[p] = (uint8_t*)f->data[p] + (long long)start * f->frame_pitch[p];
+  return t;
+}
+
+// Host frames in and/or out: the batch is cut into up to kMaxChunks chunks of
+// whole frames; chunk i's H2D copy, kernel and D2H copy run on three streams
+// so that copies of neighbouring chunks overlap the kernel and each other.
+// Staging holds the whole batch (no buffer reuse, so no WAR hazards); all
+// three streams start after the work already queued on `s`, and `s` waits
+// for them before the call returns. din/dout: staged (or caller's device)
+// descriptors for frame 0.
+static int process_pipelined(h2s_ctx* c, KParams k, const h2s_frames* in, const h2s_frames* out,
+                             const h2s_frames& din, const h2s_frames& dout, int nframes, bool fast, bool vec,
+                             bool out8, hipStream_t s) {
+  const bool host_in = in->location == H2S_LOC_HOST, host_out = out->location == H2S_LOC_HOST;
+  for (hipStream_t& ps : c->ps)
+    if (!ps) {
+      hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+      if (e != hipSuccess) {
+        ps = nullptr;
+        return hip_fail(c, e, "pipeline stream");
+      }
+    }
+  for (hipEvent_t& ev : c->pev)
+    if (!ev) {
+      hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        ev = nullptr;
+        return hip_fail(c, e, "pipeline event");
+      }
+    }
+  hipStream_t s_in = c->ps[0], s_cmp = c->ps[1], s_out = c->ps[2];
+  const int per = (nframes + kMaxChunks - 1) / kMaxChunks, nch = (nframes + per - 1) / per;
+  hipEvent_t ev_start = c->pev[2 * kMaxChunks], ev_done = c->pev[2 * kMaxChunks + 1];
+  hipError_t e = hipEventRecord(ev_start, s);
+  for (hipStream_t ps : c->ps)
+    if (e == hipSuccess) e = hipStreamWaitEvent(ps, ev_start, 0);
+  if (e != hipSuccess) return hip_fail(c, e, "pipeline ordering");
+  const int slot = (int)(c->ev_count % kEvRing);
+  const char* what = nullptr;
+  for (int i = 0; i < nch && !what; i++) {
+    const int f0 = i * per, nf = nframes - f0 < per ? nframes - f0 : per;
+    const h2s_frames ci = frames_at(&din, f0), co = frames_at(&dout, f0);
+    if (host_in) {
+      const h2s_frames hi = frames_at(in, f0);
+      if ((e = copy_frames(&ci, &hi, nf, s_in)) != hipSuccess) what = "host->device copy";
+      else if ((e = hipEventRecord(c->pev[i], s_in)) != hipSuccess) what = "pipeline event";
+      else if ((e = hipStreamWaitEvent(s_cmp, c->pev[i], 0)) != hipSuccess) what = "pipeline ordering";
+      if (what) break;
+    }
+    if (c->timing && i == 0) {
+      if (!c->ev0[slot]) {
+        hipEventCreate(&c->ev0[slot]);
+        hipEventCreate(&c->ev1[slot]);
+      }
+      hipEventRecord(c->ev0[slot], s_cmp);
+    }
+    fill_geometry(&k, &ci, &co, nf);
+    if ((e = launch_chain(c, k, fast, vec, out8, nf, s_cmp)) != hipSuccess) what = "kernel launch";
+    else if (host_out) {
+      const h2s_frames ho = frames_at(out, f0);
+      if ((e = hipEventRecord(c->pev[kMaxChunks + i], s_cmp)) != hipSuccess) what = "pipeline event";
+      else if ((e = hipStreamWaitEvent(s_out, c->pev[kMaxChunks + i], 0)) != hipSuccess) what = "pipeline ordering";
+      else if ((e = copy_frames(&ho, &co, nf, s_out)) != hipSuccess) what = "device->host copy";
+    }
+  }
+  if (what) {  // drain whatever was queued before returning the caller's buffers
+    for (hipStream_t ps : c->ps) hipStreamSynchronize(ps);
+    return hip_fail(c, e, what);
+  }
+  if (c->timing) {
+    hipEventRecord(c->ev1[slot], s_cmp);
+    c->ev_count++;
+  }
+  // s waits for the last stream of the chain (D2H if any, else compute)
+  if ((e = hipEventRecord(ev_done, host_out ? s_out : s_cmp)) == hipSuccess) e = hipStreamWaitEvent(s, ev_done, 0);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    for (hipStream_t ps : c->ps) hipStreamSynchronize(ps);
+    return hip_fail(c, e, "stream synchronize");
+  }
+  return 0;
+}
+
 int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nframes, void* hip_stream) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (nframes < 0) return fail(c, H2S_E_INVALID_ARG, "nframes < 0");
@@ -741,11 +839,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
       }
       c->stage_bytes = need;
     }
-    if (host_in) {
-      din = tight(in, c->d_stage);
-      hipError_t e = copy_frames(&din, in, nframes, s);
-      if (e != hipSuccess) return hip_fail(c, e, "host->device copy");
-    }
+    if (host_in) din = tight(in, c->d_stage);
     if (host_out) dout = tight(out, (uint8_t*)c->d_stage + ((ib + 255) / 256) * 256);
   }
   fill_geometry(&k, &din, &dout, nframes);
@@ -756,6 +850,15 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   const bool fast = c->fast_enabled && tile_ok(&din, &dout, out8) && k.lut_enabled &&
                     h2s::fast_supported(k.tonemap);
   if (fast && (rc = ensure_lut_yuv(c, k, s))) return rc;
+  const bool dyn_peak = c->params.peak_detect && k.tonemap == H2S_TM_BT2390;
+  // the dynamic peak walks frames in order with a host round trip per frame,
+  // so it keeps the serial schedule
+  if ((host_in || host_out) && nframes > 1 && !dyn_peak && !c->serial_host)
+    return process_pipelined(c, k, in, out, din, dout, nframes, fast, vec, out8, s);
+  if (host_in) {
+    hipError_t e = copy_frames(&din, in, nframes, s);
+    if (e != hipSuccess) return hip_fail(c, e, "host->device copy");
+  }
   const int slot = (int)(c->ev_count % kEvRing);
   if (c->timing) {
     if (!c->ev0[slot]) {
@@ -765,7 +868,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     hipEventRecord(c->ev0[slot], s);
   }
   hipError_t e;
-  if (c->params.peak_detect && k.tonemap == H2S_TM_BT2390) {
+  if (dyn_peak) {
     if ((rc = run_dynamic_peak(c, k, fast, vec, out8, nframes, s))) return rc;
     e = hipSuccess;
   } else {

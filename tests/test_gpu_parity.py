@@ -169,6 +169,64 @@ def test_host_memory_path_equals_device_path(tm):
     assert np.array_equal(host_out.buf, dev_out.buf)
 
 
+@pytest.mark.parametrize('where', ['host_host', 'host_dev', 'dev_host'])
+def test_pipelined_host_path_equals_device_path(tm, where):
+    """h2s_process cuts a host batch into chunks (H2D | kernel | D2H on three
+    streams): 11 frames -> 6 uneven chunks, each side host or device."""
+    import torch
+    params = hdr2sdr.TonemapParams(tonemapper='reinhard', gamma=1.4)
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    F, W, H = 11, 512, 128
+    src = synth_frames('uniform', F, W, H, 10, device='cpu', seed=21)
+    want = tm(src.to_torch('cuda')).to_numpy().buf
+    src_in = src.to_numpy() if where.startswith('host') else src.to_torch('cuda')
+    dst = (hdr2sdr.FrameBatch.empty_pinned(F, W, H, 10) if where.endswith('host')
+           else hdr2sdr.FrameBatch.empty_torch(F, W, H, 10, 'cuda'))
+    tm.process(src_in, dst)
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.to_numpy().buf, want)
+
+
+def test_pipelined_host_path_padded_host_layout(tm):
+    """Host frames with row padding and frame gaps (per-plane 2D copies per
+    chunk) through the pipeline equal the tight device result."""
+    import ctypes
+    import torch
+    W, H, F, bits_out = 256, 64, 5, 10
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out)
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    src = synth_frames('smooth', F, W, H, 10, device='cpu', seed=3)
+    want = tm(src.to_torch('cuda')).to_numpy().buf
+    probe = torch.zeros(1, dtype=torch.uint8)
+    _, in_ls, in_fp = _padded_descriptor(probe, W, H, 10, 32, 4096)
+    raw_in = torch.from_numpy(_pack_padded(src.to_numpy().buf, W, H, 10, in_ls, in_fp)).pin_memory()
+    in_d, _, _ = _padded_descriptor(raw_in, W, H, 10, 32, 4096)
+    _, out_ls, out_fp = _padded_descriptor(probe, W, H, bits_out, 64, 512)
+    raw_out = torch.zeros(F * out_fp + 64, dtype=torch.uint8).pin_memory()
+    out_d, _, _ = _padded_descriptor(raw_out, W, H, bits_out, 64, 512)
+    from hdr2sdr import _abi
+    in_d.location = out_d.location = _abi.LOC_HOST
+    tm._check(tm._L.h2s_process(tm._ctx, ctypes.byref(in_d), ctypes.byref(out_d), F, None))
+    got = _unpack_padded(raw_out.numpy(), F, W, H, bits_out, out_ls, out_fp)
+    assert np.array_equal(got.reshape(F, -1), want.reshape(F, -1))
+
+
+def test_serial_host_schedule_equals_pipelined(tm, monkeypatch):
+    params = hdr2sdr.TonemapParams(tonemapper='mobius', gamma=1.0)
+    src = synth_frames('smooth', 7, 256, 64, 10, device='cpu', seed=8).to_numpy()
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    piped = tm(src).buf
+    monkeypatch.setenv('H2S_HOST_SERIAL', '1')
+    ser = hdr2sdr.Tonemapper(0, params, lattice(65))
+    try:
+        assert np.array_equal(ser(src).buf, piped)
+    finally:
+        ser.close()
+
+
 def test_batch_equals_single_frames(tm):
     import torch
     params = hdr2sdr.TonemapParams(tonemapper='mobius', gamma=0.8)
