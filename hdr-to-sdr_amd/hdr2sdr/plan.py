@@ -22,10 +22,11 @@ and its ``time=`` parsing work on it unchanged.
 from __future__ import annotations
 
 import io
+import queue
 import subprocess
 import threading
 from dataclasses import dataclass, field
-from typing import Any, Callable, Optional
+from typing import Any, Callable, Optional, Tuple
 
 import numpy as np
 
@@ -162,7 +163,7 @@ class H2SProcess:
     holds the exception)."""
 
     def __init__(self, plan: PipePlan, tonemapper: Any, batch: int = 8,
-                 popen: Callable[..., Any] = subprocess.Popen):
+                 popen: Callable[..., Any] = subprocess.Popen, depth: int = 2):
         from .frames import FrameBatch
         self.plan = plan
         self.error: Optional[BaseException] = None
@@ -172,35 +173,69 @@ class H2SProcess:
         self.enc = popen(plan.encode, stdin=subprocess.PIPE, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL)
         self.stderr = io.TextIOWrapper(self.enc.stderr, encoding='utf-8', errors='replace')
         p = plan.params
-        # page-locked staging: the pipe bytes go straight to / from HBM by DMA
-        self._src = FrameBatch.empty_pinned(self._batch, plan.width, plan.height, p.bits_in)
+        # page-locked staging: the pipe bytes go straight to / from HBM by DMA.
+        # `depth` input slots let the decoder run ahead while the GPU stage
+        # and the encoder work on earlier batches.
+        self._src = [FrameBatch.empty_pinned(self._batch, plan.width, plan.height, p.bits_in)
+                     for _ in range(max(1, int(depth)))]
         self._dst = FrameBatch.empty_pinned(self._batch, plan.width, plan.height, p.bits_out)
+        self._free: 'queue.Queue[Optional[int]]' = queue.Queue()
+        self._filled: 'queue.Queue[Optional[Tuple[int, int]]]' = queue.Queue()
+        for i in range(len(self._src)):
+            self._free.put(i)
         self.frames = 0
+        self._reader = threading.Thread(target=self._read, name='h2s-read', daemon=True)
         self._thread = threading.Thread(target=self._pump, name='h2s-pump', daemon=True)
+        self._reader.start()
         self._thread.start()
 
+    def _fail(self, e: BaseException) -> None:
+        """GPU / pipe failure: record the first error and stop both ends."""
+        if self.error is None:
+            self.error = e
+        for p in (self.dec, self.enc):
+            try:
+                p.kill()
+            except Exception:
+                pass
+
+    def _read(self) -> None:
+        """Decoder pipe -> free input slots, in order (one batch per slot)."""
+        fin = self.plan.frame_bytes_in
+        try:
+            while True:
+                slot = self._free.get()
+                if slot is None:          # the pump stopped
+                    return
+                mv = memoryview(self._src[slot].buf).cast('B')
+                got = _read_full(self.dec.stdout, mv)
+                if got // fin:
+                    self._filled.put((slot, got // fin))
+                if got < len(mv):
+                    return
+        except BaseException as e:
+            self._fail(e)
+        finally:
+            self._filled.put(None)
+
     def _pump(self) -> None:
-        fin, fout = self.plan.frame_bytes_in, self.plan.frame_bytes_out
-        src_mv = memoryview(self._src.buf).cast('B')
+        """Filled slots -> libh2s -> encoder pipe, in decode order."""
+        fout = self.plan.frame_bytes_out
         dst_mv = memoryview(self._dst.buf).cast('B')
         try:
             while True:
-                got = _read_full(self.dec.stdout, src_mv)
-                n = got // fin
-                if n:
-                    self._tm.process(self._src, self._dst, nframes=n)
-                    self.enc.stdin.write(dst_mv[:n * fout])
-                    self.frames += n
-                if got < len(src_mv):
+                item = self._filled.get()
+                if item is None:
                     break
-        except BaseException as e:  # GPU / pipe failure: stop both ends
-            self.error = e
-            for p in (self.dec, self.enc):
-                try:
-                    p.kill()
-                except Exception:
-                    pass
+                slot, n = item
+                self._tm.process(self._src[slot], self._dst, nframes=n)   # synchronous for host frames
+                self._free.put(slot)
+                self.enc.stdin.write(dst_mv[:n * fout])
+                self.frames += n
+        except BaseException as e:
+            self._fail(e)
         finally:
+            self._free.put(None)          # release a reader waiting for a slot
             try:
                 self.enc.stdin.close()
             except Exception:
@@ -224,6 +259,7 @@ class H2SProcess:
 
     def wait(self, timeout: 'float | None' = None) -> int:
         self._thread.join(timeout)
+        self._reader.join(timeout)
         self.enc.wait(timeout)
         self.dec.wait(timeout)
         rc = self.returncode

@@ -116,6 +116,23 @@ def test_pipe_executor_mechanics(tmp_path, nframes, batch):
     assert proc.frames == nframes and sum(tm.calls) == nframes
 
 
+@pytest.mark.parametrize('depth', [1, 3])
+def test_pipe_executor_keeps_frame_order_with_read_ahead(tmp_path, depth):
+    """The decoder-side reader fills up to `depth` slots ahead of the GPU
+    stage; frames still reach the encoder in decode order."""
+    pl = P.plan_from_argv(GOLD['C2']['argv'], dict(PROPS10, width=64, height=32))
+    nframes = 23
+    frames = np.arange(nframes, dtype=np.uint16)[:, None] * 8 + np.zeros((1, 64 * 32 * 3 // 2), np.uint16)
+    out = _fake_pipes(pl, tmp_path, frames)
+    tm = _FakeTonemapper()
+    proc = P.H2SProcess(pl, tm, batch=2, depth=depth)
+    list(proc.stderr)
+    assert proc.wait(timeout=60) == 0
+    got = np.fromfile(out, dtype=np.uint16).reshape(nframes, -1)
+    assert np.array_equal(got, frames)
+    assert tm.calls == [2] * 11 + [1]
+
+
 def test_pipe_executor_reports_gpu_failure(tmp_path):
     pl = P.plan_from_argv(GOLD['C2']['argv'], dict(PROPS10, width=64, height=32))
     _fake_pipes(pl, tmp_path, np.zeros((2, 64 * 32 * 3 // 2), np.uint16))
