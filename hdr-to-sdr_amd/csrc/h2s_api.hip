@@ -319,10 +319,10 @@ bool vec_ok(const h2s_frames* f, bool out8) {
   return true;
 }
 
-// tile kernel: width a multiple of 64, every row start 16-B aligned (8-B for
-// 8-bit chroma output)
+// tile kernel: at least one 64-pixel tile, every row start 16-B aligned (8-B
+// for 8-bit chroma output)
 bool tile_ok(const h2s_frames* in, const h2s_frames* out, bool out8) {
-  if (in->width % 64 || in->width < 64) return false;
+  if (in->width < 64) return false;  // width % 64 columns go to k_process (launch_chain)
   for (int p = 0; p < 3; p++) {
     if (!aligned(in->data[p], 16) || in->linesize[p] % 16 || in->frame_pitch[p] % 16) return false;
     const long long a = out8 ? (p ? 8 : 8) : 16;
@@ -628,18 +628,29 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
     F.in[p] = k.in[p], F.in_ls[p] = k.in_ls[p], F.in_fp[p] = k.in_fp[p];
     F.out[p] = k.out[p], F.out_ls[p] = k.out_ls[p], F.out_fp[p] = k.out_fp[p];
   }
-  F.W = k.W, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
+  // k_tile covers the whole 64-pixel tiles; the chroma right halo of its last
+  // tile reads the real column (F.cw stays the frame's), so the split is exact
+  const int w64 = k.W & ~63;
+  F.W = w64, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
   for (int p = 0; p < 3; p++) {
     const long long ib = (long long)(p ? k.ch : k.H) * k.in_ls[p], ob = (long long)(p ? k.ch : k.H) * k.out_ls[p];
     F.in_bytes[p] = (int)(ib < 0x7fffffff ? ib : 0x7fffffff);
     F.out_bytes[p] = (int)(ob < 0x7fffffff ? ob : 0x7fffffff);
   }
-  F.nbx = (unsigned)(k.W / 64);
+  F.nbx = (unsigned)(w64 / 64);
   F.nby = (unsigned)((k.H + 31) / 32);
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
-  return h2s::launch_fast(F, k.transfer, k.tonemap, desat, s);
+  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, s);
+  if (e != hipSuccess || w64 == k.W) return e;
+  // the columns right of the last whole tile: the generic kernel from chroma
+  // group w64/8 on (left-sited chroma needs no left neighbour)
+  KParams kt = k;
+  kt.gx0 = w64 / 8;
+  kt.ngx = (k.cw - w64 / 2 + 3) / 4;
+  kt.total = (long long)nframes * k.ch * kt.ngx;
+  return h2s::launch_process(kt, vec, out8, s);
 }
 
 // libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):

@@ -132,6 +132,18 @@ def test_ragged_sizes_scalar_path(tm, W, H):
     assert_close_int(params, got, want, *src_wh)
 
 
+@pytest.mark.parametrize('bits_out', [10, 8])
+@pytest.mark.parametrize('W,H', [(80, 34), (352, 64), (720, 48), (1440, 36)])
+def test_tile_plus_tail_widths(tm, W, H, bits_out):
+    """Widths that are not a multiple of 64 with 16-byte aligned rows: whole
+    64-pixel tiles go through k_tile and the remaining columns through
+    k_process from the same chroma group on (the seam sits at W & ~63)."""
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out)
+    for kind in ('uniform', 'smooth'):
+        got, want, src_wh = run_both(tm, params, kind, W, H, nframes=2)
+        assert_close_int(params, got, want, *src_wh)
+
+
 def test_lut_disabled_closed_form(tm):
     params = hdr2sdr.TonemapParams(tonemapper='hable', lut_enabled=False)
     got, want, src_wh = run_both(tm, params, 'ramp', 128, 64)
