@@ -543,7 +543,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->k_r = (float)(yo + mrcr * co);
   F->k_g = (float)(yo + (mgcb + mgcr) * co);
   F->k_b = (float)(yo + mbcb * co);
-  (void)ys;
+  F->y_off_c = (float)yo;
+  F->c_mid = (float)(128 << sh);
   for (int odd = 0; odd < 2; odd++) {
     const double d = odd ? 8.0 : 4.0;
     F->a_rv[odd] = (float)(mrcr * cs / d);

@@ -69,6 +69,7 @@ struct FastParams {
   float ys, k_r, k_g, k_b;
   float a_rv[2], a_gv[2], a_gu[2], a_bu[2];
   float log2_lin_scale;
+  float y_off_c, c_mid;            // k_tile staging: Y' = Y*ys + y_off_c, chroma centred on c_mid
   // S2
   float lr, lg, lb, desat;
   float rein_p, rein_k;

@@ -65,17 +65,22 @@ __device__ __forceinline__ float pq_exact(const FastParams& F, float e) {
   return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + F.log2_lin_scale);
 }
 
-// table form: 4 full-rate VALU + 2 half-rate + one LDS read, no transcendentals.
-// ESC = PQ_SEG when the caller already scaled e by PQ_SEG (folded into the
-// Y'CbCr->R'G'B' constants), 1 otherwise.
-template <int ESC>
-__device__ __forceinline__ float pq_table(const float4* tab, float e) {
-  const float u = ESC == 1 ? __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * 0.99999994f) * (float)PQ_SEG
-                           : __builtin_amdgcn_fmed3f(e, 0.0f, PQ_EMAX * (float)PQ_SEG * 0.99999994f);
-  const float4 c = tab[(int)u];
+// Zero-segment form used by k_tile: the LDS table holds a zero segment at
+// index 0 and segment i of pq_tab at i+1, and the caller passes
+// u = E*PQ_SEG + 1 (the +1 is folded into the staged luma).  v_cvt_u32_f32
+// saturates negatives to 0, so E < 0 reads the zero segment (EOTF = 0) with no
+// clamp; at and past PQZ_LIM the value is garbage and the caller takes the
+// exact path.  The byte offset is formed with a 16-bit shift (full rate; bits
+// 31:16 are written as zero on gfx950, and the index fits 12 bits).
+__device__ __forceinline__ float pq_z(const float4* tab, float u) {
+  unsigned off;
+  asm("v_cvt_u32_f32 %0, %1\n\tv_lshlrev_b16 %0, 4, %0" : "=v"(off) : "v"(u));
+  const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + off);
   const float t = __builtin_amdgcn_fractf(u);
   return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
 }
+// staged E (table-segment units, +1) at and above which pq_z is invalid
+constexpr float PQZ_LIM = PQ_EMAX * (float)PQ_SEG + 1.0f;
 
 // S1 transfer to linear (units of npl), specialised
 // returns true (wave-uniform) when some lane of the wave took the exact PQ
@@ -85,13 +90,15 @@ template <int TRC, int ESC = 1>
 __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
                                           float& r, float& g, float& b) {
   if (TRC == 0) {
-    r = pq_table<ESC>(pq_lds, er), g = pq_table<ESC>(pq_lds, eg), b = pq_table<ESC>(pq_lds, eb);
+    // E arrives as E*PQ_SEG + 1 (pq_z)
+    static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
+    r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
     const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
-    constexpr float EL = PQ_EMAX * (float)ESC, EI = 1.0f / (float)ESC;
-    if (__builtin_amdgcn_ballot_w64(emax >= EL)) {  // rare: extreme out-of-gamut codes
-      r = er >= EL ? pq_exact(F, er * EI) : r;
-      g = eg >= EL ? pq_exact(F, eg * EI) : g;
-      b = eb >= EL ? pq_exact(F, eb * EI) : b;
+    constexpr float EI = 1.0f / (float)PQ_SEG;
+    if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {  // rare: extreme out-of-gamut codes
+      r = er >= PQZ_LIM ? pq_exact(F, (er - 1.0f) * EI) : r;
+      g = eg >= PQZ_LIM ? pq_exact(F, (eg - 1.0f) * EI) : g;
+      b = eb >= PQZ_LIM ? pq_exact(F, (eb - 1.0f) * EI) : b;
       return true;
     }
     return false;
@@ -124,8 +131,8 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 //
 // BT.2390 on PQ input (TRC 0, bounded form): the EETF's first step encodes
 // sig = max(R,G,B) back to PQ, and PQ(EOTF(max E)) = max E, so e1 is the
-// input's own max code value (emax_s = max E * PQ_SEG, clamped below at the
-// code of sig = 1e-6); the final decode reads the EOTF table already in LDS.
+// input's own max code value (emax_s = max E * PQ_SEG + 1, clamped below at
+// the code of sig = 1e-6); the final decode reads the EOTF table in LDS.
 template <int TRC, int TM, int DESAT>
 __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, float& r, float& g, float& b,
                                      bool safe, float emax_s) {
@@ -133,7 +140,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
     float e1;
     if (TRC == 0 && !safe) {
-      e1 = fmaxf(emax_s * (1.0f / (float)PQ_SEG), F.b_e1min);
+      e1 = fmaxf(fmaf(emax_s, 1.0f / (float)PQ_SEG, -1.0f / (float)PQ_SEG), F.b_e1min);
     } else {  // exact PQ encode: HLG input, or the wave met the exact EOTF path
       const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
       e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
@@ -147,7 +154,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
     const float e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
     float s2;
     if (TRC == 0) {
-      s2 = pq_table<PQ_SEG>(pq_lds, e4 * (float)PQ_SEG);          // EOTF(e4) * 10000/npl
+      s2 = pq_z(pq_lds, fmaf(e4, (float)PQ_SEG, 1.0f));          // EOTF(e4) * 10000/npl
     } else {
       const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
       s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
@@ -316,7 +323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
-  __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG : 1];
+  __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
@@ -340,7 +347,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   if (t < F.eq_n) eq_lds[t] = (uint16_t)(eq0 << F.shift_out);
   for (int i = t + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
     eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
-  if (TRC == 0 && t < PQ_NSEG) pq_lds[t] = pq0;
+  if (TRC == 0 && t < PQ_NSEG) pq_lds[t + 1] = pq0;
+  if (TRC == 0 && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 
   // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block
   // (2w + (s&1), s>>1); lane = pixel (quad q = lane>>2 in a 4x4 quad grid,
@@ -355,9 +363,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const int hb = pyl ? HST : -HST;
   float* csb = csum[0] + qy * CBW + 8 * w + qx;
 
-  // hot constants live in VGPRs for the whole kernel
-  const float k_r = in_vgpr(F.k_r) * (float)ESC;
-  const float dk_g = (in_vgpr(F.k_g) - in_vgpr(F.k_r)) * (float)ESC, dk_b = (in_vgpr(F.k_b) - in_vgpr(F.k_r)) * (float)ESC;
+  // hot constants live in VGPRs for the whole kernel.  Staged samples:
+  // luma Y*ys + y_off (+1 on PQ: pq_z's zero segment), chroma centred on its
+  // midpoint code (exact), so E = Y' + a*{U,V} takes 4 FMAs
+  const float yoff = in_vgpr(F.y_off_c) * (float)ESC + (TRC == 0 ? 1.0f : 0.0f);
+  const float cmid = in_vgpr(F.c_mid);
   const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
               a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
   const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
@@ -371,17 +381,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       float v[8];
       unpack8(cur.ya, v);
       float* d = yin + (t >> 3) * YST + 8 * (t & 7);
-      // staged luma carries the red offset: Y*ys + k_r
-      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, k_r), fmaf(v[1], ysc, k_r), fmaf(v[2], ysc, k_r), fmaf(v[3], ysc, k_r));
-      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, k_r), fmaf(v[5], ysc, k_r), fmaf(v[6], ysc, k_r), fmaf(v[7], ysc, k_r));
+      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
+      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
     }
     if (t < 72) {
-      // horizontal pass (left siting, x2 scale): h[2k] = 2 c[k],
-      // h[2k+1] = c[k] + c[k+1]; exact in float
+      // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
+      // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float
       auto put = [&](const uint4 a, unsigned h, float* plane) {
         float v[9];
         unpack8(a, v);
         v[8] = (float)h;
+#pragma unroll
+        for (int k = 0; k < 9; k++) v[k] -= cmid;
         float* d = plane + (t >> 2) * HST + 16 * (t & 3);
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -406,11 +417,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
       const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
       const float ybs = ybase[oy];
-      const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, exact
+      const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
       const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
       const float er = fmaf(V, a_rv, ybs);
-      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs + dk_g));
-      const float eb = fmaf(U, a_bu, ybs + dk_b);
+      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs));
+      const float eb = fmaf(U, a_bu, ybs);
       float r, gg, bl;
       const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
       tone<TRC, TM, DESAT>(F, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
