@@ -114,8 +114,10 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_UNSUPPORTED, "bits_in must be 10 or 12 (yuv420p10le / yuv420p12le)");
   if (p->bits_out != 8 && p->bits_out != 10 && p->bits_out != 12)
     return fail(c, H2S_E_UNSUPPORTED, "bits_out must be 8, 10 or 12");
-  if (p->tonemap < H2S_TM_NONE || p->tonemap > H2S_TM_BT2390)
+  if (p->tonemap < H2S_TM_NONE || p->tonemap > H2S_TM_SPLINE)
     return fail(c, H2S_E_INVALID_ARG, "unknown tonemap operator");
+  if (p->tonemap == H2S_TM_SPLINE && !isnan(p->tm_param) && !(p->tm_param >= 0.0 && p->tm_param <= 1.5))
+    return fail(c, H2S_E_INVALID_ARG, "spline contrast (tm_param) must be in [0, 1.5]");
   if (p->mode != H2S_MODE_COMPAT8 && p->mode != H2S_MODE_NATIVE)
     return fail(c, H2S_E_INVALID_ARG, "mode must be COMPAT8 or NATIVE");
   if (p->desat_luma < 0 || p->desat_luma > 2) return fail(c, H2S_E_INVALID_ARG, "unknown desat_luma");
@@ -139,6 +141,47 @@ void bt2390_consts(double peak, double npl, KParams* k) {
 }
 
 // ST 2084 EOTF in double (normalised: 1.0 = 10000 nits)
+double pq_eotf_d(double e);
+
+// libplacebo's "spline" tone curve (tone_mapping.c, scaling PL_HDR_PQ;
+// PARITY UNPINNED: libplacebo is absent): a single-pivot
+// curve in the PQ domain, a quadratic toe below the knee and a cubic
+// shoulder above it with zero curvature at the source peak.  The knee
+// follows pick_knee with libplacebo's default constants (knee adaptation
+// 0.4, minimum 0.1, maximum 0.8, default 0.4; slope tuning 1.5, slope offset
+// 0.2).  avg_pq: the frame's average PQ level (peak detection), 0 = unknown.
+void spline_consts(double peak, double avg_pq, double npl, double contrast, KParams* k) {
+  const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
+  auto mix = [](double a, double b, double t) { return a + (b - a) * t; };
+  auto smooth = [](double e0, double e1, double x) {
+    double t = (x - e0) / (e1 - e0);
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    return t * t * (3.0 - 2.0 * t);
+  };
+  const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
+  const double dmin = pq_encode_d(0.0), dmax = pq_encode_d(npl / 10000.0);
+  double sk = avg_pq > 0.0 ? avg_pq : mix(smin, smax, kdef);
+  sk = fmin(fmax(sk, mix(smin, smax, kmin)), mix(smin, smax, kmax));
+  const double target = (sk - smin) / (smax - smin);
+  const double adapted = mix(dmin, dmax, target);
+  const double tuning = 1.0 - smooth(kmax, kdef, target) * smooth(kmin, kdef, target);
+  double dk = mix(sk, adapted, mix(kad, 1.0, tuning));
+  dk = fmin(fmax(dk, dmin), dmax);
+  double ratio = st * (smax / dmax - 1.0);
+  ratio = fmin(fmax(ratio, so), 1.0 + so);
+  const double slope = pow(pq_eotf_d(dk) / pq_eotf_d(sk), (1.0 - contrast) * ratio);
+  const double in_min = smin - sk, in_max = smax - sk, out_min = dmin - dk, out_max = dmax - dk;
+  const double tq = 2.0 * in_max * in_max;
+  k->sp_srcmin = (float)smin, k->sp_srcmax = (float)smax;
+  k->sp_kin = (float)sk, k->sp_kout = (float)dk;
+  k->sp_pa = (float)((out_min - slope * in_min) / (in_min * in_min));
+  k->sp_pb = (float)slope;
+  k->sp_qa = (float)((slope * in_max - out_max) / (in_max * tq));
+  k->sp_qb = (float)(-3.0 * (slope * in_max - out_max) / tq);
+  k->sp_qc = (float)slope;
+  k->sp_dmin = (float)dmin, k->sp_dmax = (float)dmax;
+}
+
 double pq_eotf_d(double e) {
   const double m1 = 2610.0 / 16384.0, m2 = 2523.0 / 4096.0 * 128.0, c1 = 3424.0 / 4096.0, c2 = 2413.0 / 4096.0 * 32.0,
                c3 = 2392.0 / 4096.0 * 32.0;
@@ -211,6 +254,8 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   }
   k->peak = peak;
   bt2390_consts(peak, p->npl, k);
+  k->sp_contrast = isnan(p->tm_param) ? 0.5f : (float)p->tm_param;
+  spline_consts(peak, 0.0, p->npl, k->sp_contrast, k);
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / p->npl);
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
@@ -562,6 +607,9 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->b_ks = k.b_ks, F->b_inv_1mks = k.b_inv_1mks, F->b_maxlum = k.b_maxlum;
   F->npl_1e4 = k.npl_1e4, F->e4_npl = k.e4_npl;
   F->b_e1min = (float)pq_encode_d(1e-6 * p->npl / 10000.0);
+  F->sp_srcmin = k.sp_srcmin, F->sp_srcmax = k.sp_srcmax, F->sp_kin = k.sp_kin, F->sp_kout = k.sp_kout;
+  F->sp_pa = k.sp_pa, F->sp_pb = k.sp_pb, F->sp_qa = k.sp_qa, F->sp_qb = k.sp_qb, F->sp_qc = k.sp_qc;
+  F->sp_dmin = k.sp_dmin, F->sp_dmax = k.sp_dmax;
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);
@@ -705,7 +753,9 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
       fsum += v.y;
     }
     KParams kf = k;
-    bt2390_consts(peak_update(c, fmax, fsum / npx, k.peak), c->params.npl, &kf);
+    const double peak = peak_update(c, fmax, fsum / npx, k.peak);
+    bt2390_consts(peak, c->params.npl, &kf);
+    spline_consts(peak, c->pk_avg, c->params.npl, k.sp_contrast, &kf);
     for (int p = 0; p < 3; p++) {
       kf.in[p] += f * kf.in_fp[p];
       kf.out[p] += f * kf.out_fp[p];
@@ -862,7 +912,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   const bool fast = c->fast_enabled && tile_ok(&din, &dout, out8) && k.lut_enabled &&
                     h2s::fast_supported(k.tonemap);
   if (fast && (rc = ensure_lut_yuv(c, k, s))) return rc;
-  const bool dyn_peak = c->params.peak_detect && k.tonemap == H2S_TM_BT2390;
+  const bool dyn_peak = c->params.peak_detect && (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE);
   // the dynamic peak walks frames in order with a host round trip per frame,
   // so it keeps the serial schedule
   if ((host_in || host_out) && nframes > 1 && !dyn_peak && !c->serial_host)

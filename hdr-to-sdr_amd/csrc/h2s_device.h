@@ -38,6 +38,9 @@ struct KParams {
   float mob_j, mob_a, mob_b, mob_k;  // MOBIUS
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum;  // BT2390
   float npl_1e4, e4_npl;  // npl/10000, 10000/npl
+  // SPLINE (libplacebo, PQ domain): clip range, knee, toe P, shoulder Q, output range
+  float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;
+  float sp_contrast;
   double peak;            // resolved static source peak (units of 100 nits; host side)
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
@@ -76,7 +79,8 @@ struct FastParams {
   float hable_peak_inv, hable_ef_peak_inv;
   float mob_j, mob_a, mob_b, mob_k;
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
-  float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 e1 lower bound)
+  float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 / spline e1 lower bound)
+  float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;  // SPLINE
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)
@@ -147,9 +151,25 @@ __device__ __forceinline__ float hable(float in) {
   return (in * (in * a + b * c) + d * e) * frcp(in * (in * a + b) + d * f) - e / f;
 }
 
+// libplacebo spline on a PQ-domain signal: quadratic toe below the knee,
+// cubic shoulder above it (constants: spline_consts in h2s_api.hip)
+template <class K>
+__device__ __forceinline__ float spline_pq(const K& P, float e) {
+  const float x = fminf(fmaxf(e, P.sp_srcmin), P.sp_srcmax) - P.sp_kin;
+  const float y = x > 0.0f ? fmaf(fmaf(P.sp_qa, x, P.sp_qb), x, P.sp_qc) * x : fmaf(P.sp_pa, x, P.sp_pb) * x;
+  return fminf(fmaxf(y + P.sp_kout, P.sp_dmin), P.sp_dmax);
+}
+
 // S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)
 __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g, float& b) {
   float sig, sig_orig;
+  if (P.tonemap == 8 /* SPLINE */) {
+    sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
+    const float s2 = pq_eotf(spline_pq(P, pq_encode(sig * P.npl_1e4))) * P.e4_npl;
+    const float k = s2 * frcp(sig);
+    r *= k, g *= k, b *= k;
+    return;
+  }
   if (P.tonemap == 7 /* BT2390 */) {
     sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     float e1n = (pq_encode(sig * P.npl_1e4) - P.b_srcmin) * P.b_inv_range;

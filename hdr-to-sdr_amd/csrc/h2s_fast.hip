@@ -136,7 +136,7 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 template <int TRC, int TM, int DESAT>
 __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, float& r, float& g, float& b,
                                      bool safe, float emax_s) {
-  if (TM == 7) {  // BT.2390 (no desat)
+  if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
     float e1;
     if (TRC == 0 && !safe) {
@@ -145,13 +145,18 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
       const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
       e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
     }
-    const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
-    const float t = (e1n - F.b_ks) * F.b_inv_1mks;
-    const float t2 = t * t, t3 = t2 * t;
-    const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
-                    (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
-    const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
-    const float e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
+    float e4;
+    if (TM == 7) {
+      const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
+      const float t = (e1n - F.b_ks) * F.b_inv_1mks;
+      const float t2 = t * t, t3 = t2 * t;
+      const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
+                      (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
+      const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
+      e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
+    } else {
+      e4 = spline_pq(F, e1);                            // within [PQ(0), PQ(npl)]
+    }
     float s2;
     if (TRC == 0) {
       s2 = pq_z(pq_lds, fmaf(e4, (float)PQ_SEG, 1.0f));          // EOTF(e4) * 10000/npl
@@ -529,6 +534,7 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
   X(0, 6, 1)          \
   X(0, 6, 2)          \
   X(0, 7, 0)          \
+  X(0, 8, 0)          \
   X(1, 4, 0)          \
   X(1, 4, 1)          \
   X(1, 4, 2)          \
@@ -538,9 +544,10 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
   X(1, 6, 0)          \
   X(1, 6, 1)          \
   X(1, 6, 2)          \
-  X(1, 7, 0)
+  X(1, 7, 0)          \
+  X(1, 8, 0)
 
-bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 7; }
+bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
 // desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma
 hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s) {
@@ -549,7 +556,7 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStrea
   const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb), block(256);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
-  if (tm == 7) desat = 0;
+  if (tm == 7 || tm == 8) desat = 0;
 #define K_FAST k_tile
 #define X(T, M, D)                                                   \
   if (trc == T && tm == M && desat == D) {                           \

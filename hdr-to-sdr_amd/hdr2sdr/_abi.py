@@ -23,7 +23,7 @@ H2S_E_LUT_MISSING = -5
 H2S_E_PARSE = -6
 
 TRC_PQ, TRC_HLG = 0, 1
-TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS, TM_BT2390 = range(8)
+TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS, TM_BT2390, TM_SPLINE = range(9)
 MODE_COMPAT8, MODE_NATIVE = 0, 1
 DESAT_LUMA_RGB, DESAT_LUMA_BT2020, DESAT_LUMA_BT709 = 0, 1, 2
 LOC_DEVICE, LOC_HOST = 0, 1

@@ -36,13 +36,15 @@ FFMPEG_CONVERT_FILTER = (
 )
 
 # src/utils.py:67.  The reference can only run these through libplacebo; this
-# engine runs BT.2390 natively on the GPU, Spline is not implemented.
+# engine runs both natively on the GPU (BT.2390 EETF and libplacebo's spline
+# curve, restated in libh2s; parity unpinned).
 GPU_ONLY_TONEMAPPERS = {'bt.2390', 'spline'}
 
 _TM_NAMES = {
     'none': _abi.TM_NONE, 'linear': _abi.TM_LINEAR, 'gamma': _abi.TM_GAMMA,
     'clip': _abi.TM_CLIP, 'reinhard': _abi.TM_REINHARD, 'hable': _abi.TM_HABLE,
     'mobius': _abi.TM_MOBIUS, 'bt.2390': _abi.TM_BT2390, 'bt2390': _abi.TM_BT2390,
+    'spline': _abi.TM_SPLINE,
 }
 _TRC_NAMES = {'smpte2084': _abi.TRC_PQ, 'pq': _abi.TRC_PQ,
               'arib-std-b67': _abi.TRC_HLG, 'hlg': _abi.TRC_HLG}
@@ -77,13 +79,10 @@ class TonemapParams:
     maxcll: float = 0.0
     mastering_max: float = 0.0
     desat_luma: str = 'rgb'
-    peak_detect: bool = False   # BT.2390: detected, smoothed per-frame peak (libplacebo peak_detect=1)
+    peak_detect: bool = False   # BT.2390 / spline: detected, smoothed per-frame peak (libplacebo peak_detect=1)
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
-        if tm == 'spline':
-            raise ValueError("spline tone mapping is libplacebo-only and not implemented by this engine; "
-                             "choose reinhard, mobius, hable or bt.2390")
         if tm not in _TM_NAMES:
             raise ValueError(f'unknown tonemapper {self.tonemapper!r}')
         if self.transfer not in _TRC_NAMES:
@@ -98,6 +97,9 @@ class TonemapParams:
             raise ValueError(f'bits_out must be 8, 10 or 12, got {self.bits_out}')
         if not self.gamma > 0:
             raise ValueError(f'gamma must be > 0, got {self.gamma}')
+        if tm == 'spline' and not math.isnan(self.tm_param) and not 0.0 <= self.tm_param <= 1.5:
+            # libplacebo pl_tone_map_spline: param_min 0, param_max 1.5 (contrast)
+            raise ValueError(f'spline contrast (tm_param) must be in [0, 1.5], got {self.tm_param}')
 
     # ---- construction from the reference's request ---------------------
     @classmethod
@@ -210,6 +212,10 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             tm = kv.get('tonemap', pos[0] if pos else None)
             if tm is None:
                 raise ValueError('tonemap= without an operator')
+            if is_gpu_only_tonemapper(tm):
+                # ffmpeg's vf_tonemap has no such operator (src/utils.py:62-66);
+                # the reference reaches it only through libplacebo=tonemapping=
+                raise ValueError(f'tonemap={tm} does not exist in the CPU chain (libplacebo only)')
             kw['tonemapper'] = tm.lower()
             if 'param' in kv:
                 kw['tm_param'] = float(kv['param'])
@@ -234,7 +240,7 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             kw['tonemapper'] = tm.lower()
             kw['desat'] = 0.0
             # peak_detect=1 (src/utils.py:448): per-frame detected, temporally
-            # smoothed source peak; libh2s restates it for BT.2390
+            # smoothed source peak; libh2s restates it for BT.2390 and spline
             kw['peak_detect'] = kv.get('peak_detect', '0') in ('1', 'true')
         elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
             continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)

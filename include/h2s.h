@@ -54,8 +54,10 @@ enum h2s_transfer { H2S_TRC_PQ = 0, H2S_TRC_HLG = 1 };
 
 /* Tone-map operators.  NONE..MOBIUS are ffmpeg vf_tonemap's `tonemap=`
  * values (the reference exposes reinhard/mobius/hable, src/utils.py:16);
- * BT2390 is the GPU-only operator the reference reaches through libplacebo
- * (src/utils.py:62-73, :392-471). */
+ * BT2390 and SPLINE are the GPU-only operators the reference reaches through
+ * libplacebo's `tonemapping=` (GPU_ONLY_TONEMAPPERS, src/utils.py:62-73,
+ * :392-471).  SPLINE's tm_param is libplacebo's spline contrast (NaN = 0.5,
+ * range 0..1.5). */
 enum h2s_tonemap {
   H2S_TM_NONE = 0,
   H2S_TM_LINEAR = 1,
@@ -64,7 +66,8 @@ enum h2s_tonemap {
   H2S_TM_REINHARD = 4,
   H2S_TM_HABLE = 5,
   H2S_TM_MOBIUS = 6,
-  H2S_TM_BT2390 = 7
+  H2S_TM_BT2390 = 7,
+  H2S_TM_SPLINE = 8
 };
 
 /* Output quantisation.  COMPAT8 reproduces the reference CPU chain's 8-bit
@@ -114,8 +117,9 @@ typedef struct h2s_params {
   int32_t lut_enabled;  /* 1: lut3d stage; 0: closed-form BT.2020->709     */
   int32_t mode;         /* enum h2s_mode                                   */
   int32_t desat_luma;   /* enum h2s_desat_luma                             */
-  int32_t peak_detect;  /* BT.2390 only: 1 = per-frame detected, temporally
-                         * smoothed source peak (libplacebo peak_detect=1,
+  int32_t peak_detect;  /* BT.2390 / SPLINE: 1 = per-frame detected,
+                         * temporally smoothed source peak (and, for SPLINE,
+                         * average: the knee) (libplacebo peak_detect=1,
                          * src/utils.py:448); state lives in the context   */
   int32_t reserved[4];
 } h2s_params;

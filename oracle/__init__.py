@@ -91,6 +91,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_process.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
                                      ctypes.POINTER(Frames), ctypes.POINTER(Frames), ctypes.c_int,
                                      ctypes.c_int]
+        L.oracle_process_knee.restype = ctypes.c_int
+        L.oracle_process_knee.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.POINTER(Frames), ctypes.POINTER(Frames), ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_double]
         L.oracle_debug_float.restype = ctypes.c_int
         L.oracle_debug_float.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
                                          ctypes.POINTER(Frames), ctypes.c_int, ctypes.c_void_p]
@@ -131,9 +135,10 @@ def _frames(buf: np.ndarray, width: int, height: int, bits: int) -> Frames:
 
 
 def process(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
-            nthreads: int = 0) -> np.ndarray:
+            nthreads: int = 0, avg_pq: float = 0.0) -> np.ndarray:
     """Run the restated chain over a host batch; returns the output batch
-    (uint8 for bits_out 8, else uint16)."""
+    (uint8 for bits_out 8, else uint16).  avg_pq > 0 sets the spline knee's
+    source level (peak detection)."""
     bits_in, bits_out = params.bits_in, params.bits_out
     out = np.zeros((buf.shape[0], width * height * 3 // 2), dtype=np.uint8 if bits_out == 8 else np.uint16)
     din = _frames(np.ascontiguousarray(buf), width, height, bits_in)
@@ -142,8 +147,8 @@ def process(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width
     if lattice is not None:
         lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
         n = round(lat.shape[0] ** (1 / 3))
-    rc = lib().oracle_process(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
-                              ctypes.byref(din), ctypes.byref(dout), buf.shape[0], nthreads)
+    rc = lib().oracle_process_knee(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                                   ctypes.byref(din), ctypes.byref(dout), buf.shape[0], nthreads, avg_pq)
     if rc:
         raise ValueError(f'oracle_process failed: {rc}')
     return out
@@ -222,8 +227,9 @@ class PeakState:
 
 def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
                     state: 'PeakState | None' = None) -> 'tuple[np.ndarray, list[float]]':
-    """BT.2390 with the detected peak: stats, smoothing, then each frame
-    through the chain with its own peak.  Returns (frames, peaks)."""
+    """BT.2390 / spline with the detected peak: stats, smoothing, then each
+    frame through the chain with its own peak (and, for spline, the smoothed
+    average as the knee source).  Returns (frames, peaks)."""
     state = state or PeakState()
     static_peak = resolved(params)[0]
     fmax, favg = peak_stats(params, buf, width, height)
@@ -232,7 +238,7 @@ def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarra
         pk = state.update(float(fmax[f]), float(favg[f]), static_peak)
         q = params_from(params)
         q.peak = pk
-        outs.append(process(q, lattice, np.ascontiguousarray(buf[f:f + 1]), width, height))
+        outs.append(process(q, lattice, np.ascontiguousarray(buf[f:f + 1]), width, height, avg_pq=state.avg))
         peaks.append(pk)
     return np.concatenate(outs), peaks
 

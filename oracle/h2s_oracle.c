@@ -62,6 +62,8 @@ typedef struct {
   float lin_scale;      /* 10000/npl (PQ) or 1000/npl (HLG)              */
   /* BT.2390 */
   double src_min, src_max, max_lum, ks;
+  /* SPLINE (libplacebo, PQ domain) */
+  double sp_contrast, sp_smin, sp_smax, sp_dmin, sp_dmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc;
   uint16_t eq_lut[4096];
   const float *lut;
   int lut_n;
@@ -150,12 +152,86 @@ static float bt2390_sig(const ocfg *c, float sig) {
   return st2084_eotf(e4) * (float)(10000.0 / c->p->npl);
 }
 
+/* libplacebo src/tone_mapping.c "spline" (scaling PL_HDR_PQ), restated from
+ * its published algorithm; libplacebo is absent here: PARITY UNPINNED.  The
+ * reference reaches it only through build_libplacebo_filter
+ * (src/utils.py:62-73 GPU_ONLY_TONEMAPPERS, :392-471).
+ * pick_knee: source knee = frame average PQ (peak detection) or the default
+ * 0.4 of the source range, clamped to [0.1, 0.8] of it; the target knee moves
+ * from the source knee towards the linearly rescaled point by the knee
+ * adaptation 0.4, more near the clamp ends.  Slope at the knee = (target /
+ * source knee, linear light) ^ ((1 - contrast) * clamp(1.5 (src/dst peak
+ * ratio in PQ - 1), 0.2, 1.2)).  Toe: quadratic through the origin-shifted
+ * (min, min) with that slope; shoulder: cubic through (max, max) with the
+ * slope at the knee and zero curvature at the source peak. */
+static double smoothstep_d(double e0, double e1, double x) {
+  double t = (x - e0) / (e1 - e0);
+  t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+  return t * t * (3.0 - 2.0 * t);
+}
+
+static double pq_eotf_dd(double e) {
+  if (!(e > 0.0)) return 0.0;
+  double xp = pow(e, 1.0 / (double)PQ_M2);
+  double num = xp - (double)PQ_C1 > 0.0 ? xp - (double)PQ_C1 : 0.0;
+  return pow(num / ((double)PQ_C2 - (double)PQ_C3 * xp), 1.0 / (double)PQ_M1);
+}
+
+static void spline_setup(ocfg *c, double avg_pq) {
+  const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
+  double smin = pq_encode_d(0.0), smax = pq_encode_d(c->peak * 100.0 / 10000.0);
+  double dmin = pq_encode_d(0.0), dmax = pq_encode_d(c->p->npl / 10000.0);
+  double sk = avg_pq > 0.0 ? avg_pq : smin + (smax - smin) * kdef;
+  double lo = smin + (smax - smin) * kmin, hi = smin + (smax - smin) * kmax;
+  sk = sk < lo ? lo : (sk > hi ? hi : sk);
+  double target = (sk - smin) / (smax - smin);
+  double adapted = dmin + (dmax - dmin) * target;
+  double tuning = 1.0 - smoothstep_d(kmax, kdef, target) * smoothstep_d(kmin, kdef, target);
+  double adaptation = kad + (1.0 - kad) * tuning;
+  double dk = sk + (adapted - sk) * adaptation;
+  dk = dk < dmin ? dmin : (dk > dmax ? dmax : dk);
+  double ratio = st * (smax / dmax - 1.0);
+  ratio = ratio < so ? so : (ratio > 1.0 + so ? 1.0 + so : ratio);
+  double slope = pow(pq_eotf_dd(dk) / pq_eotf_dd(sk), (1.0 - c->sp_contrast) * ratio);
+  double in_min = smin - sk, in_max = smax - sk, out_min = dmin - dk, out_max = dmax - dk;
+  c->sp_smin = smin, c->sp_smax = smax, c->sp_dmin = dmin, c->sp_dmax = dmax;
+  c->sp_kin = sk, c->sp_kout = dk;
+  c->sp_pa = (out_min - slope * in_min) / (in_min * in_min);
+  c->sp_pb = slope;
+  c->sp_qa = (slope * in_max - out_max) / (in_max * 2.0 * in_max * in_max);
+  c->sp_qb = -3.0 * (slope * in_max - out_max) / (2.0 * in_max * in_max);
+  c->sp_qc = slope;
+}
+
+/* PQ-domain curve, float per pixel like the BT.2390 path */
+static float spline_pq_f(const ocfg *c, float e) {
+  float x = e < (float)c->sp_smin ? (float)c->sp_smin : (e > (float)c->sp_smax ? (float)c->sp_smax : e);
+  x -= (float)c->sp_kin;
+  float y = x > 0.0f ? (((float)c->sp_qa * x + (float)c->sp_qb) * x + (float)c->sp_qc) * x
+                     : ((float)c->sp_pa * x + (float)c->sp_pb) * x;
+  y += (float)c->sp_kout;
+  return y < (float)c->sp_dmin ? (float)c->sp_dmin : (y > (float)c->sp_dmax ? (float)c->sp_dmax : y);
+}
+
+static float spline_sig(const ocfg *c, float sig) {
+  float e2 = spline_pq_f(c, pq_encode_f(sig * (float)(c->p->npl / 10000.0)));
+  return st2084_eotf(e2) * (float)(10000.0 / c->p->npl);
+}
+
 #define MIX(x, y, a) (x) * (1 - (a)) + (y) * (a)
 
 static rgbf tonemap_px(const ocfg *c, rgbf in) {
   rgbf o = in;
   float sig, sig_orig;
   int tm = c->p->tonemap;
+  if (tm == H2S_TM_SPLINE) {
+    sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
+    float s2 = spline_sig(c, sig);
+    o.r *= s2 / sig;
+    o.g *= s2 / sig;
+    o.b *= s2 / sig;
+    return o;
+  }
   if (tm == H2S_TM_BT2390) {
     sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
     float s2 = bt2390_sig(c, sig);
@@ -400,6 +476,9 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   c->src_max = pq_encode_d(peak * 100.0 / 10000.0);
   c->max_lum = (pq_encode_d(p->npl / 10000.0) - c->src_min) / (c->src_max - c->src_min);
   c->ks = 1.5 * c->max_lum - 0.5;
+  /* spline: contrast = tm_param (NaN -> libplacebo's default 0.5) */
+  c->sp_contrast = isnan(p->tm_param) ? 0.5 : p->tm_param;
+  spline_setup(c, 0.0);
 
   /* vf_eq create_lut (gamma only; contrast 1, brightness 0, weight 1),
    * generalised to 2^q entries for native mode. */
@@ -509,11 +588,14 @@ static void process_quad_row(const ocfg *c, const h2s_frames *in, const h2s_fram
 }
 
 /* ---- exported entry points (ctypes) ------------------------------------- */
-int oracle_process(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in,
-                   const h2s_frames *out, int nframes, int nthreads) {
+/* avg_pq > 0: the frame's (smoothed) average PQ level as the spline knee
+ * source (peak detection); 0 = the static default knee */
+int oracle_process_knee(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in,
+                        const h2s_frames *out, int nframes, int nthreads, double avg_pq) {
   ocfg c;
   int rc = resolve(&c, p, lut, lut_n);
   if (rc) return rc;
+  if (avg_pq > 0.0) spline_setup(&c, avg_pq);
   if (in->width != out->width || in->height != out->height || (in->width & 1) || (in->height & 1) ||
       in->bits != p->bits_in || out->bits != p->bits_out)
     return H2S_E_INVALID_ARG;
@@ -526,6 +608,11 @@ int oracle_process(const h2s_params *p, const float *lut, int lut_n, const h2s_f
   for (int64_t r = 0; r < rows; r++) process_quad_row(&c, in, out, (int)(r / ch), (int)(r % ch));
   (void)nthreads;
   return 0;
+}
+
+int oracle_process(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in,
+                   const h2s_frames *out, int nframes, int nthreads) {
+  return oracle_process_knee(p, lut, lut_n, in, out, nframes, nthreads, 0.0);
 }
 
 /* float RGB (planar) of frame 0 after `stage` */

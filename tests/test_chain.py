@@ -90,8 +90,15 @@ def test_tonemap_options_and_errors():
 
 
 def test_params_validation_and_struct():
+    # spline is a native operator now (libplacebo's curve, restated); its
+    # contrast param is range-checked as pl_tone_map_spline declares (0..1.5)
+    assert hdr2sdr.TonemapParams(tonemapper='Spline').to_c().tonemap == 8
     with pytest.raises(ValueError):
-        hdr2sdr.TonemapParams(tonemapper='spline')
+        hdr2sdr.TonemapParams(tonemapper='spline', tm_param=2.0)
+    with pytest.raises(ValueError):
+        hdr2sdr.TonemapParams(tonemapper='spline').filter_string()   # GPU-only, as in the reference
+    with pytest.raises(ValueError):
+        hdr2sdr.TonemapParams(tonemapper='unknown')
     with pytest.raises(ValueError):
         hdr2sdr.TonemapParams(bits_in=8)
     with pytest.raises(ValueError):
@@ -102,3 +109,14 @@ def test_params_validation_and_struct():
     # from_request: 12-bit request -> yuv420p12le, CPU chain always applies the LUT
     q = hdr2sdr.TonemapParams.from_request(Req(tonemapper='Mobius', bit_depth=12, lut_enabled=False))
     assert q.bits_out == 12 and q.lut_enabled and q.tonemapper == 'mobius'
+
+
+def test_libplacebo_spline_chain_parses_to_native_spline():
+    """build_libplacebo_filter (src/utils.py:392-471) with tonemapping=spline,
+    as the reference builds it for a GPU-only operator."""
+    chain = ('[0:v:0]format=p010,hwupload,libplacebo=w=iw:h=ih:tonemapping=spline:colorspace=bt709:'
+             'color_primaries=auto:color_trc=bt709:range=tv:peak_detect=1:format=rgba,hwdownload,format=rgba,'
+             'lut3d=file=<LUT>:interp=tetrahedral,setparams=color_primaries=bt709:color_trc=bt709:'
+             'colorspace=bt709[vout]')
+    p, lut = parse_filter_chain(chain)
+    assert p.tonemapper == 'spline' and p.peak_detect and p.desat == 0.0 and p.lut_enabled and lut == '<LUT>'

@@ -84,6 +84,9 @@ CONFIGS = {
     'C1_reinhard_33': (dict(tonemapper='reinhard', gamma=1.0, bits_out=10), 33),
     'C2_hable_65_g22': (dict(tonemapper='hable', gamma=2.2, bits_out=10), 65),
     'C3_bt2390': (dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 65),
+    'spline_65': (dict(tonemapper='spline', gamma=1.0, bits_out=10), 65),
+    'spline_hlg12_contrast1': (dict(tonemapper='spline', tm_param=1.0, bits_in=12, bits_out=12,
+                                    transfer='arib-std-b67'), 65),
     'C4_mobius': (dict(tonemapper='mobius', gamma=1.0, bits_out=10), 65),
     'C5_hlg12_hable': (dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'), 65),
     'default_8bit': (dict(tonemapper='mobius', gamma=1.0, bits_out=8), 65),
@@ -101,7 +104,8 @@ def test_configs_match_oracle(tm, cfg, kind):
 
 
 @pytest.mark.parametrize('mode', ['compat8', 'native'])
-@pytest.mark.parametrize('tmname', ['none', 'linear', 'gamma', 'clip', 'reinhard', 'hable', 'mobius', 'bt.2390'])
+@pytest.mark.parametrize('tmname', ['none', 'linear', 'gamma', 'clip', 'reinhard', 'hable', 'mobius', 'bt.2390',
+                                    'spline'])
 def test_every_operator_both_modes(tm, tmname, mode):
     params = hdr2sdr.TonemapParams(tonemapper=tmname, gamma=1.3, bits_out=10, mode=mode)
     got, want, src_wh = run_both(tm, params, 'smooth', 96, 48)
@@ -269,6 +273,7 @@ def test_errors_map_to_reference_exceptions(tm):
 @pytest.mark.parametrize('name,kw,W,H,nframes', [
     ('C2_4k_hable_g22', dict(tonemapper='hable', gamma=2.2, bits_out=10), 3840, 2160, 2),
     ('C3_4k_bt2390', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('4k_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 1),
     ('C4_4k_mobius', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 1),
     ('C5_8k_hlg12_hable', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
      7680, 4320, 1),

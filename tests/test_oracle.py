@@ -10,7 +10,8 @@ import oracle
 import hdr2sdr
 from hdr2sdr.synth import synth_frames
 
-TM = {'none': 0, 'linear': 1, 'gamma': 2, 'clip': 3, 'reinhard': 4, 'hable': 5, 'mobius': 6, 'bt.2390': 7}
+TM = {'none': 0, 'linear': 1, 'gamma': 2, 'clip': 3, 'reinhard': 4, 'hable': 5, 'mobius': 6, 'bt.2390': 7,
+      'spline': 8}
 
 
 def params(**kw):
@@ -76,6 +77,60 @@ def test_bt2390_eetf_shape():
     top = oracle.tone_curve(p, 10.0)                                        # source peak -> target peak
     assert top == pytest.approx(1.0, rel=1e-3)
     assert oracle.tone_curve(p, 100.0) == pytest.approx(top, rel=1e-6)      # clipped to source range
+
+
+# ---- libplacebo spline (PARITY UNPINNED: libplacebo absent) ----------------
+def _pq_enc(y):
+    m1, m2, c1, c2, c3 = 0.1593017578125, 78.84375, 0.8359375, 18.8515625, 18.6875
+    ym = max(y, 0.0) ** m1
+    return ((c1 + c2 * ym) / (1 + c3 * ym)) ** m2
+
+
+def _spline_ref(sig, peak=10.0, npl=100.0, contrast=0.5, avg_pq=0.0):
+    """Second, independent transcription of libplacebo's spline (pick_knee +
+    single-pivot toe/shoulder, tone_mapping.c defaults) in double."""
+    def smoothstep(e0, e1, x):
+        t = min(max((x - e0) / (e1 - e0), 0.0), 1.0)
+        return t * t * (3 - 2 * t)
+    smin, smax = _pq_enc(0.0), _pq_enc(peak / 100.0)
+    dmin, dmax = _pq_enc(0.0), _pq_enc(npl / 10000.0)
+    sk = avg_pq if avg_pq > 0 else smin + 0.4 * (smax - smin)
+    sk = min(max(sk, smin + 0.1 * (smax - smin)), smin + 0.8 * (smax - smin))
+    target = (sk - smin) / (smax - smin)
+    adapted = dmin + (dmax - dmin) * target
+    tuning = 1 - smoothstep(0.8, 0.4, target) * smoothstep(0.1, 0.4, target)
+    dk = min(max(sk + (adapted - sk) * (0.4 + 0.6 * tuning), dmin), dmax)
+    ratio = min(max(1.5 * (smax / dmax - 1), 0.2), 1.2)
+    slope = (oracle.pq_eotf_d(dk) / oracle.pq_eotf_d(sk)) ** ((1 - contrast) * ratio)
+    i0, i1, o0, o1 = smin - sk, smax - sk, dmin - dk, dmax - dk
+    x = min(max(_pq_enc(sig * npl / 10000.0), smin), smax) - sk
+    if x > 0:
+        y = ((((slope * i1 - o1) / (2 * i1 ** 3)) * x - 3 * (slope * i1 - o1) / (2 * i1 * i1)) * x + slope) * x
+    else:
+        y = ((o0 - slope * i0) / (i0 * i0) * x + slope) * x
+    e2 = min(max(y + dk, dmin), dmax)
+    return oracle.pq_eotf_d(e2) * 10000.0 / npl, sk, dk, slope
+
+
+@pytest.mark.parametrize('peak,contrast', [(10.0, 0.5), (40.0, 0.5), (10.0, 0.0), (10.0, 1.5), (2.0, 0.5)])
+def test_spline_matches_independent_transcription(peak, contrast):
+    p = params(tonemap='spline', peak=peak, tm_param=contrast)
+    for sig in (1e-4, 0.003, 0.05, 0.2, 0.5, 1.0, 2.0, 5.0, peak * 0.7, peak, peak * 3):
+        want = _spline_ref(sig, peak=peak, contrast=contrast)[0]
+        assert oracle.tone_curve(p, sig) == pytest.approx(want, rel=2e-4, abs=1e-6), sig
+
+
+def test_spline_shape():
+    p = params(tonemap='spline')                     # peak 10 (1000 nits), contrast 0.5
+    xs = np.geomspace(1e-4, 10.0, 300)
+    ys = [oracle.tone_curve(p, float(x)) for x in xs]
+    assert all(b >= a - 1e-7 for a, b in zip(ys, ys[1:]))               # monotone
+    assert ys[-1] == pytest.approx(1.0, rel=1e-4)                        # source peak -> SDR white
+    assert oracle.tone_curve(p, 100.0) == pytest.approx(ys[-1], rel=1e-6)  # clipped to the source range
+    _, sk, dk, slope = _spline_ref(1.0)
+    assert 0.0 < dk < sk and 0.0 < slope < 1.0       # compressive knee on a 1000-nit source
+    # contrast 1 -> the slope exponent is 0: unit PQ-domain slope at the knee
+    assert _spline_ref(1.0, contrast=1.0)[3] == pytest.approx(1.0)
 
 
 # ---- S7: vf_eq create_lut ---------------------------------------------------

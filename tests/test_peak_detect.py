@@ -71,11 +71,12 @@ def sequence(W=256, H=128):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('tmname', ['bt.2390', 'spline'])   # spline also takes its knee from the average
 @pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])     # fast path and generic kernel
-def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H):
+def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname):
     from test_gpu_parity import assert_close_int, lattice
     buf = sequence(W, H)
-    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0)
     tm = hdr2sdr.Tonemapper(0, params, lattice(65))
     got = []
     for a, b in ((0, 2), (2, 5), (5, 6)):            # the state carries across calls
