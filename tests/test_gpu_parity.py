@@ -359,3 +359,41 @@ def test_padded_strides_and_frame_gaps(tm, bits_out):
     got = _unpack_padded(raw_out.cpu().numpy(), F, W, H, bits_out, out_ls, out_fp).astype(np.int64)
     assert np.array_equal(got, got_tight)
     assert_close_int(params, got, want, W, H)
+
+
+def test_concurrent_contexts_on_threads_match_serial():
+    """The ABI contract (include/h2s.h): any thread may call
+    libh2s, one context per worker, no global mutable state.  Four threads,
+    each with its own context and operator, process host batches at the same
+    time (the ctypes calls release the GIL); every result equals the same
+    context's serial result."""
+    import threading
+    W, H = 256, 128
+    cfgs = [dict(tonemapper='hable', gamma=2.2), dict(tonemapper='mobius'), dict(tonemapper='spline'),
+            dict(tonemapper='bt.2390', bits_out=8)]
+    srcs = [synth_frames(k, 3, W, H, 10, device='cpu', seed=50 + i).to_numpy()
+            for i, k in enumerate(('smooth', 'uniform', 'ramp', 'edges'))]
+    ctxs = [hdr2sdr.Tonemapper(0, hdr2sdr.TonemapParams(**c), lattice(65)) for c in cfgs]
+    outs = [[None] * 5 for _ in ctxs]
+    errs = []
+
+    def work(i):
+        try:
+            for r in range(5):
+                dst = hdr2sdr.FrameBatch.empty_numpy(3, W, H, ctxs[i].params.bits_out)
+                ctxs[i].process(srcs[i], dst)
+                outs[i][r] = dst.buf.copy()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(len(ctxs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=60)
+    assert not errs, errs
+    for i, c in enumerate(ctxs):
+        dst = hdr2sdr.FrameBatch.empty_numpy(3, W, H, c.params.bits_out)
+        c.process(srcs[i], dst)
+        for r in range(5):
+            assert np.array_equal(outs[i][r], dst.buf), (cfgs[i], r)
+        c.close()

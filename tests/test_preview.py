@@ -153,3 +153,28 @@ def test_gpu_preview_rejects_non_8bit_context():
                                       _abi.LOC_HOST, None)
     assert rc == _abi.H2S_E_INVALID_ARG
     tm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('kind,seed', [('smooth', 21), ('ramp', 5)])
+def test_gpu_lut_chain_tracks_legacy_gamut_chain(kind, seed):
+    """The reference's colour-correctness safety net,
+    TestLutReproducesLegacyGamutMath (test/smoke_test.py:264-343), on the
+    product path: one 960x540 HDR10 frame through libh2s as the reference
+    renders it to PNG, once with FFMPEG_CONVERT_FILTER (reinhard, gamma 1,
+    65^3 tetrahedral LUT: k_tile) and once with FFMPEG_FILTER_LEGACY_NO_LUT
+    (closed-form BT.2020->709 + clip), sampled on the same 21x21 grid
+    (w // 20 steps); max per-channel difference <= 12/255 (_TOLERANCE,
+    :300).  The reference measured a worst case of 10/255 on real content."""
+    W, H = 960, 540
+    src = synth_frames(kind, 1, W, H, 10, device='cpu', seed=seed).to_numpy()
+    imgs = []
+    for lut in (False, True):
+        with PV.Previewer(0, tonemapper='reinhard', lut_enabled=lut, lattice=_lat()) as pv:
+            imgs.append(pv.convert(src, 'iw', 'ih').astype(int))
+    legacy, with_lut = imgs
+    xs = np.arange(0, W, max(1, W // 20))
+    ys = np.arange(0, H, max(1, H // 20))
+    d = np.abs(legacy[ys][:, xs] - with_lut[ys][:, xs])
+    assert d.max() <= 12, f'LUT chain differs from the legacy chain by up to {d.max()}/255'
+    assert np.abs(legacy - with_lut).mean() < 3.0        # and close on average, not only on the grid
