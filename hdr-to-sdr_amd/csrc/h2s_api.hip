@@ -602,6 +602,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->rein_p = k.rein_p, F->rein_k = k.rein_k;
   F->hable_peak_inv = k.hable_peak_inv;
   F->hable_ef_peak_inv = (0.02f / 0.30f) * k.hable_peak_inv;
+  F->hable_ka = (float)(2.1 / 15.0 * (double)k.hable_peak_inv);
+  F->hable_kb = (float)(0.25 / 15.0 * (double)k.hable_peak_inv);
   F->mob_j = k.mob_j, F->mob_a = k.mob_a, F->mob_b = k.mob_b, F->mob_k = k.mob_k;
   F->b_srcmin = k.b_srcmin, F->b_range = k.b_range, F->b_inv_range = k.b_inv_range;
   F->b_ks = k.b_ks, F->b_inv_1mks = k.b_inv_1mks, F->b_maxlum = k.b_maxlum;

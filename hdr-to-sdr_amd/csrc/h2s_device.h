@@ -77,6 +77,7 @@ struct FastParams {
   float lr, lg, lb, desat;
   float rein_p, rein_k;
   float hable_peak_inv, hable_ef_peak_inv;
+  float hable_ka, hable_kb;        // 0.14 / hable(peak), (1/60) / hable(peak): hable(x)/x = (0.14 x + 1/60) / D(x)
   float mob_j, mob_a, mob_b, mob_k;
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
   float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 / spline e1 lower bound)

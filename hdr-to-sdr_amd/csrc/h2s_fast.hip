@@ -204,10 +204,12 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
   float k;
   if (TM == 4) {
     k = F.rein_k * frcp(sig + F.rein_p);
-  } else if (TM == 5) {  // (num hpi - ef hpi den) / (den sig): one reciprocal
-    const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
-    const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
-    k = fmaf(num, F.hable_peak_inv, -F.hable_ef_peak_inv * den) * frcp(den * sig);
+  } else if (TM == 5) {
+    // hable(x) = N/D - e/f with 15 N - D = x (2.1 x + 0.25) (the constant
+    // terms cancel: d*e*15 = d*f), so hable(x)/x = (0.14 x + 1/60) / D:
+    // one reciprocal, no cancellation, and sig drops out of the gain
+    const float den = fmaf(sig, fmaf(sig, 0.15f, 0.50f), 0.06f);
+    k = fmaf(sig, F.hable_ka, F.hable_kb) * frcp(den);
   } else {
     const float m = F.mob_k * (sig + F.mob_a) * frcp((sig + F.mob_b) * sig);
     k = sig <= F.mob_j ? 1.0f : m;
