@@ -612,6 +612,21 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->sp_srcmin = k.sp_srcmin, F->sp_srcmax = k.sp_srcmax, F->sp_kin = k.sp_kin, F->sp_kout = k.sp_kout;
   F->sp_pa = k.sp_pa, F->sp_pb = k.sp_pb, F->sp_qa = k.sp_qa, F->sp_qb = k.sp_qb, F->sp_qc = k.sp_qc;
   F->sp_dmin = k.sp_dmin, F->sp_dmax = k.sp_dmax;
+  {
+    const double seg = h2s::PQ_SEG, smin = k.b_srcmin, range = k.b_range, ks = k.b_ks, ml = k.b_maxlum;
+    const double R = range * seg, C = smin * seg + 1.0;
+    // (2t^3-3t^2+1) ks + (t^3-2t^2+t)(1-ks) + (-2t^3+3t^2) ml as a3 t^3 + a2 t^2 + a1 t + a0
+    const double a3 = ks + 1.0 - 2.0 * ml, a2 = -ks - 2.0 + 3.0 * ml, a1 = 1.0 - ks, a0 = ks;
+    F->b_e1a = k.b_inv_range, F->b_e1b = (float)(-smin * (double)k.b_inv_range);
+    F->b_ta = k.b_inv_1mks, F->b_tb = (float)(-ks * (double)k.b_inv_1mks);
+    F->b_c3 = (float)(R * a3), F->b_c2 = (float)(R * a2), F->b_c1 = (float)(R * a1), F->b_c0 = (float)(R * a0 + C);
+    F->b_lr = (float)R, F->b_lc = (float)C;
+    F->b_thr = ks < 1.0 ? (float)ks : 2.0f;   // ks >= 1: the knee is never reached
+    F->sp_qa_u = (float)(seg * k.sp_qa), F->sp_qb_u = (float)(seg * k.sp_qb), F->sp_qc_u = (float)(seg * k.sp_qc);
+    F->sp_pa_u = (float)(seg * k.sp_pa), F->sp_pb_u = (float)(seg * k.sp_pb);
+    F->sp_k_u = (float)(seg * k.sp_kout + 1.0);
+    F->sp_umin = (float)(seg * k.sp_dmin + 1.0), F->sp_umax = (float)(seg * k.sp_dmax + 1.0);
+  }
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);

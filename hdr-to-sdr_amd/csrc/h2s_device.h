@@ -82,6 +82,11 @@ struct FastParams {
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
   float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 / spline e1 lower bound)
   float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;  // SPLINE
+  // PQ-input forms that land directly on pq_z's table coordinate u = e*PQ_SEG + 1:
+  // BT.2390: e1n = med3(e1*e1a + e1b), t = e1n*ta + tb, u = c3..c0 Horner (knee) or e1n*lr + lc
+  float b_e1a, b_e1b, b_ta, b_tb, b_c3, b_c2, b_c1, b_c0, b_lr, b_lc, b_thr;
+  // spline: u = Horner(x) with the coefficients and kout scaled by PQ_SEG, clamped to [umin, umax]
+  float sp_qa_u, sp_qb_u, sp_qc_u, sp_pa_u, sp_pb_u, sp_k_u, sp_umin, sp_umax;
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)

@@ -145,22 +145,37 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
       const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
       e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
     }
-    float e4;
-    if (TM == 7) {
-      const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
-      const float t = (e1n - F.b_ks) * F.b_inv_1mks;
-      const float t2 = t * t, t3 = t2 * t;
-      const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
-                      (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
-      const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
-      e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
-    } else {
-      e4 = spline_pq(F, e1);                            // within [PQ(0), PQ(npl)]
-    }
     float s2;
     if (TRC == 0) {
-      s2 = pq_z(pq_lds, fmaf(e4, (float)PQ_SEG, 1.0f));          // EOTF(e4) * 10000/npl
+      // the curve straight into pq_z's table coordinate u = e4*PQ_SEG + 1:
+      // the output scale and offset are folded into the polynomial
+      // coefficients on the host (resolve_fast)
+      float u;
+      if (TM == 7) {   // BT.2390 Hermite knee as one cubic in t, Horner form
+        const float e1n = __builtin_amdgcn_fmed3f(fmaf(e1, F.b_e1a, F.b_e1b), 0.0f, 1.0f);
+        const float t = fmaf(e1n, F.b_ta, F.b_tb);
+        const float uk = fmaf(fmaf(fmaf(F.b_c3, t, F.b_c2), t, F.b_c1), t, F.b_c0);
+        u = e1n > F.b_thr ? uk : fmaf(e1n, F.b_lr, F.b_lc);
+      } else {         // spline: cubic shoulder / quadratic toe around the knee
+        const float x = __builtin_amdgcn_fmed3f(e1, F.sp_srcmin, F.sp_srcmax) - F.sp_kin;
+        const float uq = fmaf(fmaf(fmaf(F.sp_qa_u, x, F.sp_qb_u), x, F.sp_qc_u), x, F.sp_k_u);
+        const float up = fmaf(fmaf(F.sp_pa_u, x, F.sp_pb_u), x, F.sp_k_u);
+        u = __builtin_amdgcn_fmed3f(x > 0.0f ? uq : up, F.sp_umin, F.sp_umax);
+      }
+      s2 = pq_z(pq_lds, u);                                       // EOTF(e4) * 10000/npl
     } else {
+      float e4;
+      if (TM == 7) {
+        const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
+        const float t = (e1n - F.b_ks) * F.b_inv_1mks;
+        const float t2 = t * t, t3 = t2 * t;
+        const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
+                        (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
+        const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
+        e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
+      } else {
+        e4 = spline_pq(F, e1);                            // within [PQ(0), PQ(npl)]
+      }
       const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
       s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
     }
