@@ -179,7 +179,7 @@ int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
 int h2s_debug_float(h2s_ctx *ctx, const h2s_frames *in, int stage,
                     float *out_rgb, int out_location, void *hip_stream);
 
-/* ---- dynamic peak (params.peak_detect, BT.2390) --------------------------
+/* ---- dynamic peak (params.peak_detect, BT.2390 / spline) -----------------
  * h2s_peak_reset: forget the smoothing state (a new sequence / scene cut).
  * h2s_peak_state: the smoothed PQ-domain max / average after the last
  *   processed frame, the source peak (units of npl) it gave, and the number
