@@ -208,7 +208,10 @@ def main():
                 ('C5', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
                  7680, 4320, 4, 65),
                 # the reference's other GPU-only operator (libplacebo spline), C3's shape
-                ('C3_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 16, 65)):
+                ('C3_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
+                # C3 with libplacebo's peak_detect=1 (src/utils.py:448): stats launch, host IIR, one tile launch
+                ('C3_dyn', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=True, maxcll=4000.0),
+                 3840, 2160, 16, 65)):
             p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
             t_ = hdr2sdr.Tonemapper(local, p_, hdr2sdr.generate_lattice(lut_n))
             src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)

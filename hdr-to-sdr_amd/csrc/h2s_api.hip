@@ -58,6 +58,10 @@ struct h2s_ctx {
   // dynamic peak (params.peak_detect): per-frame stats buffer + IIR state
   float2* d_peak = nullptr;
   size_t peak_cap = 0;
+  h2s::CurveConsts* d_curve = nullptr;    // one curve record per frame of a dynamic-peak launch
+  size_t curve_cap = 0;
+  std::vector<h2s::CurveConsts> h_curve;  // host side of the last upload (alive until it completes)
+  hipEvent_t curve_ev = nullptr;          // recorded after the launch that reads d_curve
   double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
   long long pk_frames = 0;
   std::string err;
@@ -501,6 +505,8 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
   if (c->d_peak) hipFree(c->d_peak);
+  if (c->d_curve) hipFree(c->d_curve);
+  if (c->curve_ev) hipEventDestroy(c->curve_ev);
   for (int i = 0; i < kEvRing; i++) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
@@ -574,6 +580,31 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   return 0;
 }
 
+// BT.2390 / spline constants in the fast kernel's folded form (per launch, or
+// per frame under dynamic peak detection)
+static void curve_fast(const KParams& k, h2s::CurveConsts* cc) {
+  cc->b_srcmin = k.b_srcmin, cc->b_range = k.b_range, cc->b_inv_range = k.b_inv_range;
+  cc->b_ks = k.b_ks, cc->b_inv_1mks = k.b_inv_1mks, cc->b_maxlum = k.b_maxlum;
+  cc->sp_srcmin = k.sp_srcmin, cc->sp_srcmax = k.sp_srcmax, cc->sp_kin = k.sp_kin, cc->sp_kout = k.sp_kout;
+  cc->sp_pa = k.sp_pa, cc->sp_pb = k.sp_pb, cc->sp_qa = k.sp_qa, cc->sp_qb = k.sp_qb, cc->sp_qc = k.sp_qc;
+  cc->sp_dmin = k.sp_dmin, cc->sp_dmax = k.sp_dmax;
+  {
+    const double seg = h2s::PQ_SEG, smin = k.b_srcmin, range = k.b_range, ks = k.b_ks, ml = k.b_maxlum;
+    const double R = range * seg, C = smin * seg + 1.0;
+    // (2t^3-3t^2+1) ks + (t^3-2t^2+t)(1-ks) + (-2t^3+3t^2) ml as a3 t^3 + a2 t^2 + a1 t + a0
+    const double a3 = ks + 1.0 - 2.0 * ml, a2 = -ks - 2.0 + 3.0 * ml, a1 = 1.0 - ks, a0 = ks;
+    cc->b_e1a = k.b_inv_range, cc->b_e1b = (float)(-smin * (double)k.b_inv_range);
+    cc->b_ta = k.b_inv_1mks, cc->b_tb = (float)(-ks * (double)k.b_inv_1mks);
+    cc->b_c3 = (float)(R * a3), cc->b_c2 = (float)(R * a2), cc->b_c1 = (float)(R * a1), cc->b_c0 = (float)(R * a0 + C);
+    cc->b_lr = (float)R, cc->b_lc = (float)C;
+    cc->b_thr = ks < 1.0 ? (float)ks : 2.0f;   // ks >= 1: the knee is never reached
+    cc->sp_qa_u = (float)(seg * k.sp_qa), cc->sp_qb_u = (float)(seg * k.sp_qb), cc->sp_qc_u = (float)(seg * k.sp_qc);
+    cc->sp_pa_u = (float)(seg * k.sp_pa), cc->sp_pb_u = (float)(seg * k.sp_pb);
+    cc->sp_k_u = (float)(seg * k.sp_kout + 1.0);
+    cc->sp_umin = (float)(seg * k.sp_dmin + 1.0), cc->sp_umax = (float)(seg * k.sp_dmax + 1.0);
+  }
+}
+
 // FastParams from the resolved KParams (same constants, scales folded)
 static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   memset(F, 0, sizeof(*F));
@@ -605,28 +636,9 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->hable_ka = (float)(2.1 / 15.0 * (double)k.hable_peak_inv);
   F->hable_kb = (float)(0.25 / 15.0 * (double)k.hable_peak_inv);
   F->mob_j = k.mob_j, F->mob_a = k.mob_a, F->mob_b = k.mob_b, F->mob_k = k.mob_k;
-  F->b_srcmin = k.b_srcmin, F->b_range = k.b_range, F->b_inv_range = k.b_inv_range;
-  F->b_ks = k.b_ks, F->b_inv_1mks = k.b_inv_1mks, F->b_maxlum = k.b_maxlum;
   F->npl_1e4 = k.npl_1e4, F->e4_npl = k.e4_npl;
   F->b_e1min = (float)pq_encode_d(1e-6 * p->npl / 10000.0);
-  F->sp_srcmin = k.sp_srcmin, F->sp_srcmax = k.sp_srcmax, F->sp_kin = k.sp_kin, F->sp_kout = k.sp_kout;
-  F->sp_pa = k.sp_pa, F->sp_pb = k.sp_pb, F->sp_qa = k.sp_qa, F->sp_qb = k.sp_qb, F->sp_qc = k.sp_qc;
-  F->sp_dmin = k.sp_dmin, F->sp_dmax = k.sp_dmax;
-  {
-    const double seg = h2s::PQ_SEG, smin = k.b_srcmin, range = k.b_range, ks = k.b_ks, ml = k.b_maxlum;
-    const double R = range * seg, C = smin * seg + 1.0;
-    // (2t^3-3t^2+1) ks + (t^3-2t^2+t)(1-ks) + (-2t^3+3t^2) ml as a3 t^3 + a2 t^2 + a1 t + a0
-    const double a3 = ks + 1.0 - 2.0 * ml, a2 = -ks - 2.0 + 3.0 * ml, a1 = 1.0 - ks, a0 = ks;
-    F->b_e1a = k.b_inv_range, F->b_e1b = (float)(-smin * (double)k.b_inv_range);
-    F->b_ta = k.b_inv_1mks, F->b_tb = (float)(-ks * (double)k.b_inv_1mks);
-    F->b_c3 = (float)(R * a3), F->b_c2 = (float)(R * a2), F->b_c1 = (float)(R * a1), F->b_c0 = (float)(R * a0 + C);
-    F->b_lr = (float)R, F->b_lc = (float)C;
-    F->b_thr = ks < 1.0 ? (float)ks : 2.0f;   // ks >= 1: the knee is never reached
-    F->sp_qa_u = (float)(seg * k.sp_qa), F->sp_qb_u = (float)(seg * k.sp_qb), F->sp_qc_u = (float)(seg * k.sp_qc);
-    F->sp_pa_u = (float)(seg * k.sp_pa), F->sp_pb_u = (float)(seg * k.sp_pb);
-    F->sp_k_u = (float)(seg * k.sp_kout + 1.0);
-    F->sp_umin = (float)(seg * k.sp_dmin + 1.0), F->sp_umax = (float)(seg * k.sp_dmax + 1.0);
-  }
+  curve_fast(k, F);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);
@@ -684,9 +696,22 @@ static int prepare(h2s_ctx* c, KParams* k) {
   return 0;
 }
 
-// one launch of the chain over nframes frames described by k
+// the generic kernel over the columns right of the last whole 64-pixel tile
+// (left-sited chroma needs no left neighbour, so the seam is exact)
+static hipError_t launch_tail(const KParams& k, int nframes, bool vec, bool out8, hipStream_t s) {
+  const int w64 = k.W & ~63;
+  KParams kt = k;
+  kt.gx0 = w64 / 8;
+  kt.ngx = (k.cw - w64 / 2 + 3) / 4;
+  kt.total = (long long)nframes * k.ch * kt.ngx;
+  return h2s::launch_process(kt, vec, out8, s);
+}
+
+// one launch of the chain over nframes frames described by k.  cvf: per-frame
+// curve records (dynamic peak, fast kernel); tail = false leaves the ragged
+// right columns to the caller
 static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
-                               hipStream_t s) {
+                               hipStream_t s, const h2s::CurveConsts* cvf = nullptr, bool tail = true) {
   if (!fast) return h2s::launch_process(k, vec, out8, s);
   FastParams F;
   resolve_fast(c, k, &F);
@@ -707,16 +732,11 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.nby = (unsigned)((k.H + 31) / 32);
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
+  F.cv_frames = cvf;
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
   hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, s);
-  if (e != hipSuccess || w64 == k.W) return e;
-  // the columns right of the last whole tile: the generic kernel from chroma
-  // group w64/8 on (left-sited chroma needs no left neighbour)
-  KParams kt = k;
-  kt.gx0 = w64 / 8;
-  kt.ngx = (k.cw - w64 / 2 + 3) / 4;
-  kt.total = (long long)nframes * k.ch * kt.ngx;
-  return h2s::launch_process(kt, vec, out8, s);
+  if (e != hipSuccess || w64 == k.W || !tail) return e;
+  return launch_tail(k, nframes, vec, out8, s);
 }
 
 // libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):
@@ -743,7 +763,10 @@ static double peak_update(h2s_ctx* c, double fmax, double favg, double static_pe
 }
 
 // statistics for every frame in one launch, then the frames in order, each
-// with the BT.2390 constants of its smoothed peak
+// with the BT.2390 / spline constants of its smoothed peak.  The fast kernel
+// takes every frame's curve in one launch (a record per frame, selected by the
+// tile's frame index), so the chip stays full; the generic kernel and the
+// ragged tail columns go frame by frame.
 static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
   const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
   if (need > c->peak_cap) {
@@ -762,6 +785,11 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
   const double npx = (double)k.W * k.H;
+  std::vector<KParams> kfs(nframes, k);
+  if (fast) {
+    if (c->curve_ev && (e = hipEventSynchronize(c->curve_ev)) != hipSuccess) return hip_fail(c, e, "curve upload");
+    c->h_curve.resize(nframes);
+  }
   for (int f = 0; f < nframes; f++) {
     double fmax = 0.0, fsum = 0.0;
     for (int b = 0; b < h2s::PEAK_BLOCKS; b++) {
@@ -769,17 +797,43 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
       fmax = v.x > fmax ? v.x : fmax;
       fsum += v.y;
     }
-    KParams kf = k;
+    KParams& kf = kfs[f];
     const double peak = peak_update(c, fmax, fsum / npx, k.peak);
     bt2390_consts(peak, c->params.npl, &kf);
     spline_consts(peak, c->pk_avg, c->params.npl, k.sp_contrast, &kf);
+    if (fast) curve_fast(kf, &c->h_curve[f]);
     for (int p = 0; p < 3; p++) {
       kf.in[p] += f * kf.in_fp[p];
       kf.out[p] += f * kf.out_fp[p];
     }
     kf.nframes = 1;
     kf.total = (long long)kf.ch * kf.ngx;
-    if ((e = launch_chain(c, kf, fast, vec, out8, 1, s)) != hipSuccess) return hip_fail(c, e, "kernel launch");
+  }
+  if (fast) {
+    if ((size_t)nframes > c->curve_cap) {
+      if (c->d_curve) hipFree(c->d_curve);
+      c->d_curve = nullptr;
+      c->curve_cap = 0;
+      if (hipMalloc((void**)&c->d_curve, (size_t)nframes * sizeof(h2s::CurveConsts)) != hipSuccess) {
+        c->d_curve = nullptr;
+        return fail(c, H2S_E_OOM, "curve records allocation failed");
+      }
+      c->curve_cap = nframes;
+    }
+    if (!c->curve_ev && (e = hipEventCreateWithFlags(&c->curve_ev, hipEventDisableTiming)) != hipSuccess) {
+      c->curve_ev = nullptr;
+      return hip_fail(c, e, "curve event");
+    }
+    e = hipMemcpyAsync(c->d_curve, c->h_curve.data(), (size_t)nframes * sizeof(h2s::CurveConsts),
+                       hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
+    if (e == hipSuccess) e = hipEventRecord(c->curve_ev, s);
+    if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+    if ((k.W & 63) == 0) return 0;
+  }
+  for (int f = 0; f < nframes; f++) {
+    e = fast ? launch_tail(kfs[f], 1, vec, out8, s) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
+    if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   }
   return 0;
 }

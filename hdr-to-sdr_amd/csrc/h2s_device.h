@@ -57,9 +57,22 @@ struct KParams {
   int gx0;  // first column group this launch covers (tail launches)
 };
 
+// Constants of the PQ-domain curves (BT.2390 / spline) in the fast kernel's
+// folded form.  They are the only parameters that change from frame to frame
+// under dynamic peak detection, so a launch can take one record per frame.
+struct CurveConsts {
+  float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum;  // BT.2390, HLG input
+  // PQ-input forms that land directly on pq_z's table coordinate u = e*PQ_SEG + 1:
+  // BT.2390: e1n = med3(e1*e1a + e1b), t = e1n*ta + tb, u = c3..c0 Horner (knee) or e1n*lr + lc
+  float b_e1a, b_e1b, b_ta, b_tb, b_c3, b_c2, b_c1, b_c0, b_lr, b_lc, b_thr;
+  float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;  // SPLINE
+  // spline: u = Horner(x) with the coefficients and kout scaled by PQ_SEG, clamped to [umin, umax]
+  float sp_qa_u, sp_qb_u, sp_qc_u, sp_pa_u, sp_pb_u, sp_k_u, sp_umin, sp_umax;
+};
+
 // Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
 // with every scale folded into constants.
-struct FastParams {
+struct FastParams : CurveConsts {
   int W, H, cw, ch;                // luma / chroma geometry (W % 64 == 0)
   unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
   int tpb;                         // tiles walked by one block (k_tile prefetches tile i+1 during tile i)
@@ -79,14 +92,10 @@ struct FastParams {
   float hable_peak_inv, hable_ef_peak_inv;
   float hable_ka, hable_kb;        // 0.14 / hable(peak), (1/60) / hable(peak): hable(x)/x = (0.14 x + 1/60) / D(x)
   float mob_j, mob_a, mob_b, mob_k;
-  float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum, npl_1e4, e4_npl;
+  float npl_1e4, e4_npl;
   float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 / spline e1 lower bound)
-  float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;  // SPLINE
-  // PQ-input forms that land directly on pq_z's table coordinate u = e*PQ_SEG + 1:
-  // BT.2390: e1n = med3(e1*e1a + e1b), t = e1n*ta + tb, u = c3..c0 Horner (knee) or e1n*lr + lc
-  float b_e1a, b_e1b, b_ta, b_tb, b_c3, b_c2, b_c1, b_c0, b_lr, b_lc, b_thr;
-  // spline: u = Horner(x) with the coefficients and kout scaled by PQ_SEG, clamped to [umin, umax]
-  float sp_qa_u, sp_qb_u, sp_qc_u, sp_pa_u, sp_pb_u, sp_k_u, sp_umin, sp_umax;
+  const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
+                                   // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)

@@ -134,8 +134,8 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // input's own max code value (emax_s = max E * PQ_SEG + 1, clamped below at
 // the code of sig = 1e-6); the final decode reads the EOTF table in LDS.
 template <int TRC, int TM, int DESAT>
-__device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, float& r, float& g, float& b,
-                                     bool safe, float emax_s) {
+__device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds, float& r,
+                                     float& g, float& b, bool safe, float emax_s) {
   if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
     float e1;
@@ -152,29 +152,29 @@ __device__ __forceinline__ void tone(const FastParams& F, const float4* pq_lds, 
       // coefficients on the host (resolve_fast)
       float u;
       if (TM == 7) {   // BT.2390 Hermite knee as one cubic in t, Horner form
-        const float e1n = __builtin_amdgcn_fmed3f(fmaf(e1, F.b_e1a, F.b_e1b), 0.0f, 1.0f);
-        const float t = fmaf(e1n, F.b_ta, F.b_tb);
-        const float uk = fmaf(fmaf(fmaf(F.b_c3, t, F.b_c2), t, F.b_c1), t, F.b_c0);
-        u = e1n > F.b_thr ? uk : fmaf(e1n, F.b_lr, F.b_lc);
+        const float e1n = __builtin_amdgcn_fmed3f(fmaf(e1, C.b_e1a, C.b_e1b), 0.0f, 1.0f);
+        const float t = fmaf(e1n, C.b_ta, C.b_tb);
+        const float uk = fmaf(fmaf(fmaf(C.b_c3, t, C.b_c2), t, C.b_c1), t, C.b_c0);
+        u = e1n > C.b_thr ? uk : fmaf(e1n, C.b_lr, C.b_lc);
       } else {         // spline: cubic shoulder / quadratic toe around the knee
-        const float x = __builtin_amdgcn_fmed3f(e1, F.sp_srcmin, F.sp_srcmax) - F.sp_kin;
-        const float uq = fmaf(fmaf(fmaf(F.sp_qa_u, x, F.sp_qb_u), x, F.sp_qc_u), x, F.sp_k_u);
-        const float up = fmaf(fmaf(F.sp_pa_u, x, F.sp_pb_u), x, F.sp_k_u);
-        u = __builtin_amdgcn_fmed3f(x > 0.0f ? uq : up, F.sp_umin, F.sp_umax);
+        const float x = __builtin_amdgcn_fmed3f(e1, C.sp_srcmin, C.sp_srcmax) - C.sp_kin;
+        const float uq = fmaf(fmaf(fmaf(C.sp_qa_u, x, C.sp_qb_u), x, C.sp_qc_u), x, C.sp_k_u);
+        const float up = fmaf(fmaf(C.sp_pa_u, x, C.sp_pb_u), x, C.sp_k_u);
+        u = __builtin_amdgcn_fmed3f(x > 0.0f ? uq : up, C.sp_umin, C.sp_umax);
       }
       s2 = pq_z(pq_lds, u);                                       // EOTF(e4) * 10000/npl
     } else {
       float e4;
       if (TM == 7) {
-        const float e1n = fmaxf(fminf((e1 - F.b_srcmin) * F.b_inv_range, 1.0f), 0.0f);
-        const float t = (e1n - F.b_ks) * F.b_inv_1mks;
+        const float e1n = fmaxf(fminf((e1 - C.b_srcmin) * C.b_inv_range, 1.0f), 0.0f);
+        const float t = (e1n - C.b_ks) * C.b_inv_1mks;
         const float t2 = t * t, t3 = t2 * t;
-        const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * F.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - F.b_ks) +
-                        (-2.0f * t3 + 3.0f * t2) * F.b_maxlum;
-        const float e2 = (F.b_ks < 1.0f && e1n > F.b_ks) ? p : e1n;
-        e4 = fmaxf(e2 * F.b_range + F.b_srcmin, 0.0f);   // <= source max <= 1
+        const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * C.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - C.b_ks) +
+                        (-2.0f * t3 + 3.0f * t2) * C.b_maxlum;
+        const float e2 = (C.b_ks < 1.0f && e1n > C.b_ks) ? p : e1n;
+        e4 = fmaxf(e2 * C.b_range + C.b_srcmin, 0.0f);   // <= source max <= 1
       } else {
-        e4 = spline_pq(F, e1);                            // within [PQ(0), PQ(npl)]
+        e4 = spline_pq(C, e1);                            // within [PQ(0), PQ(npl)]
       }
       const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
       s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
@@ -286,6 +286,19 @@ struct TileRegs {
 struct TileGeo {
   int f, px0, py0, cx0, cy0;
 };
+
+// frame f's curve record: a constant-address-space load with a block-uniform
+// index, so the compiler emits scalar (s_load) reads
+__device__ __forceinline__ CurveConsts curve_of(const CurveConsts* frames, int f) {
+  typedef __attribute__((address_space(4))) const float cfloat;
+  constexpr int n = (int)(sizeof(CurveConsts) / sizeof(float));
+  cfloat* src = (cfloat*)frames + __builtin_amdgcn_readfirstlane(f) * n;
+  CurveConsts r;
+  float* dst = reinterpret_cast<float*>(&r);
+#pragma unroll
+  for (int i = 0; i < n; i++) dst[i] = src[i];
+  return r;
+}
 
 __device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) {
   const unsigned bx = tile % F.nbx, bt = tile / F.nbx;
@@ -425,6 +438,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       put(cur.va, cur.vh, hrow[1]);
     }
     const TileGeo g = geo;
+    // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
+    // frame, read through the scalar cache; the frame index is block-uniform)
+    CurveConsts cv = F;
+    if ((TM == 7 || TM == 8) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
       tile_next(F, geo);
@@ -446,7 +463,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const float eb = fmaf(U, a_bu, ybs);
       float r, gg, bl;
       const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
-      tone<TRC, TM, DESAT>(F, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
+      tone<TRC, TM, DESAT>(F, cv, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
       const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));

@@ -72,7 +72,7 @@ def sequence(W=256, H=128):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('tmname', ['bt.2390', 'spline'])   # spline also takes its knee from the average
-@pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])     # fast path and generic kernel
+@pytest.mark.parametrize('W,H', [(256, 128), (192, 96), (200, 96)])   # fast path (blocks within / across frames), + tail
 def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname):
     from test_gpu_parity import assert_close_int, lattice
     buf = sequence(W, H)
