@@ -260,33 +260,21 @@ hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s) 
 // clamp(max(E), 0, 1) exactly, so no transcendental is needed.  Chroma is
 // taken nearest (the statistic is an estimate).  grid = (PEAK_BLOCKS, frames);
 // partial[f * PEAK_BLOCKS + b] = (max, sum) over the rows b, b + PEAK_BLOCKS, ...
+// one pixel's PQ-domain max(R,G,B) from its integer codes (nearest chroma)
 template <int TRC>
-__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial) {
-  const int f = blockIdx.y, b = blockIdx.x;
-  float mx = 0.0f, sm = 0.0f;
-  for (int y = b; y < P.H; y += gridDim.x) {
-    const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
-    const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
-    const uint16_t* vr = reinterpret_cast<const uint16_t*>(P.in[2] + f * P.in_fp[2] + (y >> 1) * P.in_ls[2]);
-    float rs = 0.0f;
-    for (int x = threadIdx.x; x < P.W; x += blockDim.x) {
-      const float Y = (float)yr[x] * P.y_scale + P.y_off;
-      const float cb = (float)ur[x >> 1] * P.c_scale + P.c_off, cr = (float)vr[x >> 1] * P.c_scale + P.c_off;
-      const float er = Y + P.m_rcr * cr, eg = Y + P.m_gcb * cb + P.m_gcr * cr, eb = Y + P.m_bcb * cb;
-      float m;
-      if (TRC == 0) {
-        m = clamp01(fmaxf(fmaxf(er, eg), eb));
-      } else {
-        const float r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), bl = hlg_inv_oetf(eb);
-        const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * bl;
-        const float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
-        m = clamp01(pq_encode(fmaxf(fmaxf(r, g), bl) * w * P.npl_1e4));
-      }
-      mx = fmaxf(mx, m);
-      rs += m;
-    }
-    sm += rs;
-  }
+__device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned uc, unsigned vc) {
+  const float Y = (float)yc * P.y_scale + P.y_off;
+  const float cb = (float)uc * P.c_scale + P.c_off, cr = (float)vc * P.c_scale + P.c_off;
+  const float er = Y + P.m_rcr * cr, eg = Y + P.m_gcb * cb + P.m_gcr * cr, eb = Y + P.m_bcb * cb;
+  if (TRC == 0) return clamp01(fmaxf(fmaxf(er, eg), eb));
+  const float r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), bl = hlg_inv_oetf(eb);
+  const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * bl;
+  const float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
+  return clamp01(pq_encode(fmaxf(fmaxf(r, g), bl) * w * P.npl_1e4));
+}
+
+// block (max, sum) reduction; thread 0 writes the record
+__device__ __forceinline__ void peak_reduce(float mx, float sm, float2* out) {
   __shared__ float smx[256], ssm[256];
   smx[threadIdx.x] = mx, ssm[threadIdx.x] = sm;
   __syncthreads();
@@ -297,13 +285,92 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) partial[f * gridDim.x + b] = make_float2(smx[0], ssm[0]);
+  if (threadIdx.x == 0) *out = make_float2(smx[0], ssm[0]);
+}
+
+// generic form: any width / alignment, 2-byte loads
+template <int TRC>
+__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial) {
+  const int f = blockIdx.y, b = blockIdx.x;
+  float mx = 0.0f, sm = 0.0f;
+  for (int y = b; y < P.H; y += gridDim.x) {
+    const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
+    const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
+    const uint16_t* vr = reinterpret_cast<const uint16_t*>(P.in[2] + f * P.in_fp[2] + (y >> 1) * P.in_ls[2]);
+    float rs = 0.0f;
+    for (int x = threadIdx.x; x < P.W; x += blockDim.x) {
+      const float m = peak_px<TRC>(P, yr[x], ur[x >> 1], vr[x >> 1]);
+      mx = fmaxf(mx, m);
+      rs += m;
+    }
+    sm += rs;
+  }
+  peak_reduce(mx, sm, &partial[f * gridDim.x + b]);
+}
+
+// streaming form (W % 8 == 0, 16-byte luma / 8-byte chroma alignment): each
+// thread takes 8-pixel chunks (one 16-byte luma load, one 8-byte load per
+// chroma plane), two chunks per iteration so two loads per plane are in flight
+template <int TRC>
+__global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial) {
+  const int f = blockIdx.y;
+  const int cpr = P.W >> 3;                       // chunks per row
+  const int nch = P.H * cpr, stride = gridDim.x * 256;
+  const uint8_t* y0 = P.in[0] + f * P.in_fp[0];
+  const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
+  const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
+  float mx = 0.0f, sm = 0.0f;
+  auto chunk = [&](int i, uint4& ya, uint2& ua, uint2& va) {
+    const int y = i / cpr, cx = i - y * cpr;
+    ya = reinterpret_cast<const uint4*>(y0 + y * P.in_ls[0])[cx];
+    ua = reinterpret_cast<const uint2*>(u0 + (y >> 1) * P.in_ls[1])[cx];
+    va = reinterpret_cast<const uint2*>(v0 + (y >> 1) * P.in_ls[2])[cx];
+  };
+  auto fold = [&](const uint4 ya, const uint2 ua, const uint2 va) {
+    const unsigned yy[8] = {ya.x & 0xffff, ya.x >> 16, ya.y & 0xffff, ya.y >> 16,
+                            ya.z & 0xffff, ya.z >> 16, ya.w & 0xffff, ya.w >> 16};
+    const unsigned uu[4] = {ua.x & 0xffff, ua.x >> 16, ua.y & 0xffff, ua.y >> 16};
+    const unsigned vv[4] = {va.x & 0xffff, va.x >> 16, va.y & 0xffff, va.y >> 16};
+    float rs = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
+      mx = fmaxf(mx, m);
+      rs += m;
+    }
+    sm += rs;
+  };
+  int i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < nch; i += 2 * stride) {
+    uint4 ya0, ya1;
+    uint2 ua0, ua1, va0, va1;
+    chunk(i, ya0, ua0, va0);
+    chunk(i + stride, ya1, ua1, va1);
+    fold(ya0, ua0, va0);
+    fold(ya1, ua1, va1);
+  }
+  if (i < nch) {
+    uint4 ya;
+    uint2 ua, va;
+    chunk(i, ya, ua, va);
+    fold(ya, ua, va);
+  }
+  peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
 }
 
 constexpr int PEAK_BLOCKS_K = 64;
 hipError_t launch_peak_stats(const KParams& P, float2* partial, hipStream_t s) {
   const dim3 grid(PEAK_BLOCKS_K, P.nframes);
-  if (P.transfer == 1)
+  auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
+  const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
+                   al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
+                   al(P.in_fp[1], 8) && al((long long)(uintptr_t)P.in[2], 8) && al(P.in_ls[2], 8) &&
+                   al(P.in_fp[2], 8);
+  if (vec && P.transfer == 1)
+    hipLaunchKernelGGL(k_peak_stats_v<1>, grid, dim3(256), 0, s, P, partial);
+  else if (vec)
+    hipLaunchKernelGGL(k_peak_stats_v<0>, grid, dim3(256), 0, s, P, partial);
+  else if (P.transfer == 1)
     hipLaunchKernelGGL(k_peak_stats<1>, grid, dim3(256), 0, s, P, partial);
   else
     hipLaunchKernelGGL(k_peak_stats<0>, grid, dim3(256), 0, s, P, partial);

@@ -110,3 +110,23 @@ def test_gpu_peak_reset_restarts_the_sequence():
     assert tm.peak_state()['frames'] == 1
     assert np.array_equal(out_a.buf, out_b.buf)
     tm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W,H', [(204, 96), (256, 64)])     # scalar stats + tail, streaming stats
+def test_gpu_dynamic_peak_hlg12(W, H):
+    """12-bit HLG source (C5's input format) under peak detection: the stats
+    take the inverse OETF + OOTF path; both stats kernels and the tail."""
+    from test_gpu_parity import assert_close_int, lattice
+    buf = synth_frames('smooth', 4, W, H, 12, device='cpu', seed=77).to_numpy().buf
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, transfer='arib-std-b67',
+                                   bits_in=12, bits_out=12)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 12)
+    dst = hdr2sdr.FrameBatch.empty_numpy(4, W, H, 12)
+    tm.process(src, dst)
+    state = tm.peak_state()
+    tm.close()
+    want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert state['frames'] == 4 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
+    assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
