@@ -259,6 +259,7 @@ def test_batch_equals_single_frames(tm):
 def test_errors_map_to_reference_exceptions(tm):
     params = hdr2sdr.TonemapParams(tonemapper='hable')
     tm.set_params(params)
+    tm.set_lut(lattice(65))      # so the bits mismatch, not LUT_MISSING, is hit
     src = synth_frames('uniform', 1, 64, 32, 10, device='cpu').to_torch('cuda')
     bad = hdr2sdr.FrameBatch.empty_torch(1, 64, 32, 8, 'cuda')   # bits mismatch
     with pytest.raises(ValueError):
@@ -267,6 +268,29 @@ def test_errors_map_to_reference_exceptions(tm):
     with pytest.raises(FileNotFoundError):
         fresh(src)
     fresh.close()
+
+
+def test_empty_and_negative_batches(tm):
+    """nframes=0 is a no-op that leaves dst untouched (an empty pipe read in
+    the planner); nframes<0 is INVALID_ARG -> ValueError, like every other
+    impossible request (src/ffmpeg_command.py:240-245)."""
+    import torch
+    tm.set_params(hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=10))
+    tm.set_lut(lattice(65))
+    src = synth_frames('smooth', 2, 128, 64, 10, device='cpu').to_torch('cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(2, 128, 64, 10, 'cuda')
+    dst.buf.fill_(0x1234)
+    tm.process(src, dst, nframes=0)
+    torch.cuda.synchronize()
+    assert bool((dst.buf == 0x1234).all())
+    with pytest.raises(ValueError):
+        tm.process(src, dst, nframes=-1)
+    with pytest.raises(ValueError):
+        tm.process(src, dst, nframes=3)          # more than the batch holds
+    tm.process(src, dst, nframes=1)              # only frame 0 is written
+    torch.cuda.synchronize()
+    assert not bool((dst.buf[0] == 0x1234).all())
+    assert bool((dst.buf[1] == 0x1234).all())
 
 
 # ---- BASELINE.json full sizes (the oracle is OpenMP C: whole frames in ~1 s)
