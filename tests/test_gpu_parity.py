@@ -89,6 +89,8 @@ CONFIGS = {
                                     transfer='arib-std-b67'), 65),
     'C4_mobius': (dict(tonemapper='mobius', gamma=1.0, bits_out=10), 65),
     'C5_hlg12_hable': (dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'), 65),
+    'pq12_reinhard_12': (dict(tonemapper='reinhard', gamma=1.0, bits_in=12, bits_out=12), 65),
+    'pq12_bt2390_10': (dict(tonemapper='bt.2390', gamma=1.0, bits_in=12, bits_out=10), 65),
     'default_8bit': (dict(tonemapper='mobius', gamma=1.0, bits_out=8), 65),
     'gamma05_8bit': (dict(tonemapper='hable', gamma=0.5, bits_out=8), 65),
 }
