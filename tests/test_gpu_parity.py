@@ -138,13 +138,15 @@ def test_ragged_sizes_scalar_path(tm, W, H):
     assert_close_int(params, got, want, *src_wh)
 
 
+@pytest.mark.parametrize('bits_in,transfer', [(10, 'smpte2084'), (12, 'arib-std-b67')])
 @pytest.mark.parametrize('bits_out', [10, 8])
 @pytest.mark.parametrize('W,H', [(80, 34), (352, 64), (720, 48), (1440, 36)])
-def test_tile_plus_tail_widths(tm, W, H, bits_out):
+def test_tile_plus_tail_widths(tm, W, H, bits_out, bits_in, transfer):
     """Widths that are not a multiple of 64 with 16-byte aligned rows: whole
     64-pixel tiles go through k_tile and the remaining columns through
     k_process from the same chroma group on (the seam sits at W & ~63)."""
-    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out)
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_in=bits_in, bits_out=bits_out,
+                                   transfer=transfer)
     for kind in ('uniform', 'smooth'):
         got, want, src_wh = run_both(tm, params, kind, W, H, nframes=2)
         assert_close_int(params, got, want, *src_wh)
