@@ -10,7 +10,10 @@ collective: weak scaling); the only collectives are the RCCL broadcast of the
 LUT lattice at start-up and a MAX all-reduce of the elapsed time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B]
-For N > 1 the driver launches one process per GPU with torch.distributed.run.
+For N > 1 the driver launches one process per GPU with torch.distributed.run;
+a plain ``python bench.py --gpus N`` (no WORLD_SIZE in the environment)
+starts that launcher itself, as a child process, before touching the GPU.
+--dry-run exercises the launch and collectives only (no GPU; gloo on CPU).
 """
 from __future__ import annotations
 
@@ -32,7 +35,8 @@ def parse_args():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--frames', type=int, default=16, help='frames per rank per step')
+    ap.add_argument('--frames', type=int, default=64,
+                    help='frames per rank per step (C4: 512 frames / 8 GPUs = 64)')
     ap.add_argument('--width', type=int, default=3840)
     ap.add_argument('--height', type=int, default=2160)
     ap.add_argument('--kind', default='smooth', help='synthetic content (smooth|uniform|ramp|edges)')
@@ -45,7 +49,29 @@ def parse_args():
     ap.add_argument('--mode', default='compat8')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline budget (0 = skip)')
     ap.add_argument('--no-alt', action='store_true', help='skip the uniform-content secondary run')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launch + collectives only, no GPU work (CPU test of the multi-rank flow)')
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(gpus: int) -> int:
+    """--gpus N without a torch.distributed launcher around us: start one
+    (torch.distributed.run, N local ranks, rendezvous on 127.0.0.1) as a child
+    process and return its exit code.  Called before anything initialises the
+    GPU; the parent never execs."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes', '1', '--nproc-per-node', str(gpus),
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_baseline(params, lattice, width, height, budget_s):
@@ -92,8 +118,48 @@ def pmc_traffic(workload):
     return None
 
 
+def dry_run(args, world, rank):
+    """The multi-rank flow without the GPU: gloo process group, the
+    params + lattice broadcast, the SUM / MAX reduction; rank 0 prints the
+    JSON line shape with n_gpus / world_size as the collectives saw them."""
+    import torch.distributed as dist
+
+    import hdr2sdr
+    from hdr2sdr.dist import broadcast_setup, reduce_run, shard_range
+    if world > 1:
+        dist.init_process_group('gloo')
+    params = hdr2sdr.TonemapParams(tonemapper=args.tonemapper, gamma=args.gamma)
+    n = 17
+    lat = hdr2sdr.generate_lattice(n) if rank == 0 else None
+    if world > 1:
+        params, lat = broadcast_setup(params if rank == 0 else None, lat, n)
+        seen = dist.get_world_size()
+    else:
+        seen = 1
+    a, b = shard_range(world * args.frames, world, rank)
+    px, cks, el = (b - a) * args.width * args.height, 0, 0.001 * (rank + 1)
+    if world > 1:
+        px, cks, el = reduce_run(px, cks, el)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({'dry_run': True, 'n_gpus': args.gpus, 'world_size': seen, 'pixels': px,
+                          'max_elapsed_s': el, 'gamma': params.gamma, 'lattice_sum': float(lat.sum())}), flush=True)
+
+
 def main():
     args = parse_args()
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or '1')
+    rank = int(os.environ.get('RANK', '0'))
+    if world != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required',
+              file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
     import torch
     import torch.distributed as dist
 
@@ -101,8 +167,6 @@ def main():
     from hdr2sdr.dist import broadcast_setup, frame_checksum, reduce_run, shard_range
     from hdr2sdr.synth import synth_frames
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
     # one process per GPU; H2S_BENCH_DEVICE / H2S_DIST_BACKEND=gloo only let a
     # single-GPU box rehearse the multi-rank flow (ranks sharing one device)
     local = int(os.environ.get('H2S_BENCH_DEVICE', os.environ.get('LOCAL_RANK', '0')))
@@ -113,6 +177,7 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
+    seen_world = dist.get_world_size() if world > 1 else 1
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
@@ -249,6 +314,7 @@ def main():
         'value': round(value, 1),
         'unit': 'Mpixel/s',
         'n_gpus': world,
+        'world_size': seen_world,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': round(el / args.steps * 1e3, 4),
@@ -263,7 +329,8 @@ def main():
             'frames_per_rank_per_step': B,
             'width': W, 'height': H,
             'content': args.kind,
-            'parallelism': f'frame-sharded x{world} (RCCL LUT broadcast only)',
+            'parallelism': f'frame-sharded x{world} ({backend if world > 1 else "single rank"}; '
+                           f'params + LUT broadcast only)',
             'alt_content': alt,
             'other_configs': other,
             'host_path': host_path,

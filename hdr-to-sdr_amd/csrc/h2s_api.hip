@@ -17,7 +17,8 @@ namespace h2s {
 hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
 hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
 bool fast_supported(int tonemap);
-hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s);
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s, int dbg = 0);
+hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
                             long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
@@ -72,6 +73,9 @@ struct h2s_ctx {
   // their own streams (two DMA directions overlap the kernel and each other)
   hipStream_t ps[3] = {};
   hipEvent_t pev[2 * kMaxChunks + 2] = {};
+  bool launched = false;         // work queued since the last set_params / set_lut drain
+  float2* d_chr = nullptr;       // BICUBIC chroma: one frame's per-pixel (Cb, Cr)
+  size_t chr_cap = 0;
 };
 
 namespace {
@@ -128,20 +132,48 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
   if (!(p->gamma > 0) || !isfinite(p->gamma)) return fail(c, H2S_E_INVALID_ARG, "gamma must be > 0");
   if (!(p->npl > 0) || !isfinite(p->npl)) return fail(c, H2S_E_INVALID_ARG, "npl must be > 0");
   if (!(p->desat >= 0)) return fail(c, H2S_E_INVALID_ARG, "desat must be >= 0");
+  if (p->chroma_filter != H2S_CHROMA_BOX && p->chroma_filter != H2S_CHROMA_BICUBIC)
+    return fail(c, H2S_E_INVALID_ARG, "unknown chroma_filter");
+  if (p->dither != H2S_DITHER_NONE && p->dither != H2S_DITHER_ORDERED)
+    return fail(c, H2S_E_INVALID_ARG, "unknown dither");
+  if (p->expand != H2S_EXPAND_SHIFT && p->expand != H2S_EXPAND_REPLICATE)
+    return fail(c, H2S_E_INVALID_ARG, "unknown expand");
+  if (p->pipeline < H2S_PIPE_AUTO || p->pipeline > H2S_PIPE_LIBPLACEBO)
+    return fail(c, H2S_E_INVALID_ARG, "unknown pipeline");
+  if (p->pipeline == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
+    return fail(c, H2S_E_UNSUPPORTED,
+                "libplacebo pipeline: only bt.2390 / spline are restated (libplacebo's hable/mobius/reinhard "
+                "curves differ from vf_tonemap's)");
+  if (!isnan(p->knee_offset) && !(p->knee_offset >= 0.5 && p->knee_offset <= 2.0))
+    return fail(c, H2S_E_INVALID_ARG, "knee_offset must be in [0.5, 2] (libplacebo's range)");
+  if (!isnan(p->target_white) && !(p->target_white > 0 && isfinite(p->target_white)))
+    return fail(c, H2S_E_INVALID_ARG, "target_white must be > 0");
+  if (!isnan(p->target_black) && !(p->target_black >= 0 && isfinite(p->target_black)))
+    return fail(c, H2S_E_INVALID_ARG, "target_black must be >= 0");
+  if (!isnan(p->target_black) && !isnan(p->target_white) && !(p->target_black < p->target_white))
+    return fail(c, H2S_E_INVALID_ARG, "target_black must be below target_white");
   return 0;
 }
 
-// BT.2390 EETF constants for a source peak (units of 100 nits) and target npl
-void bt2390_consts(double peak, double npl, KParams* k) {
+// BT.2390 EETF constants (libplacebo tone_mapping.c bt2390) for a source
+// peak (units of 100 nits) and the SDR target [k->t_black, k->t_white] nits:
+// knee ks = (1 + offset) maxLum - offset, black-point adaptation exponent
+// bp = min(1 / minLum, 4) and gain 1 / (1 + minLum / maxLum (1 - maxLum)^bp)
+void bt2390_consts(double peak, KParams* k) {
   const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
-  const double ml = (pq_encode_d(npl / 10000.0) - smin) / (smax - smin);
-  const double ks = 1.5 * ml - 0.5;
+  const double ml = (pq_encode_d(k->t_white / 10000.0) - smin) / (smax - smin);
+  const double mn = k->t_black > 0.0 ? (pq_encode_d(k->t_black / 10000.0) - smin) / (smax - smin) : 0.0;
+  const double ks = (1.0 + k->knee_off) * ml - k->knee_off;
+  const double bp = mn > 0.0 ? fmin(1.0 / mn, 4.0) : 4.0;
   k->b_srcmin = (float)smin;
   k->b_range = (float)(smax - smin);
   k->b_inv_range = (float)(1.0 / (smax - smin));
   k->b_ks = (float)ks;
   k->b_inv_1mks = (float)(1.0 / (1.0 - ks));
   k->b_maxlum = (float)ml;
+  k->b_minlum = (float)mn;
+  k->b_bp = (float)bp;
+  k->b_gain = (float)(ml < 1.0 ? 1.0 / (1.0 + mn / ml * pow(1.0 - ml, bp)) : 1.0);
 }
 
 // ST 2084 EOTF in double (normalised: 1.0 = 10000 nits)
@@ -154,7 +186,7 @@ double pq_eotf_d(double e);
 // follows pick_knee with libplacebo's default constants (knee adaptation
 // 0.4, minimum 0.1, maximum 0.8, default 0.4; slope tuning 1.5, slope offset
 // 0.2).  avg_pq: the frame's average PQ level (peak detection), 0 = unknown.
-void spline_consts(double peak, double avg_pq, double npl, double contrast, KParams* k) {
+void spline_consts(double peak, double avg_pq, double contrast, KParams* k) {
   const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
   auto mix = [](double a, double b, double t) { return a + (b - a) * t; };
   auto smooth = [](double e0, double e1, double x) {
@@ -163,7 +195,7 @@ void spline_consts(double peak, double avg_pq, double npl, double contrast, KPar
     return t * t * (3.0 - 2.0 * t);
   };
   const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
-  const double dmin = pq_encode_d(0.0), dmax = pq_encode_d(npl / 10000.0);
+  const double dmin = pq_encode_d(k->t_black / 10000.0), dmax = pq_encode_d(k->t_white / 10000.0);
   double sk = avg_pq > 0.0 ? avg_pq : mix(smin, smax, kdef);
   sk = fmin(fmax(sk, mix(smin, smax, kmin)), mix(smin, smax, kmax));
   const double target = (sk - smin) / (smax - smin);
@@ -257,11 +289,27 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
     k->mob_k = (b * b + 2.0f * b * j + j * j) / (b - a);
   }
   k->peak = peak;
-  bt2390_consts(peak, p->npl, k);
+  // pipeline and SDR target (oracle resolve: the CPU chain's curve output is
+  // relative to npl with no black; libplacebo targets PL_COLOR_SDR_WHITE =
+  // 203 nits at PL_COLOR_SDR_CONTRAST = 1000:1)
+  k->pipe = p->pipeline != H2S_PIPE_AUTO ? p->pipeline
+                                         : (p->tonemap == H2S_TM_BT2390 || p->tonemap == H2S_TM_SPLINE ? h2s::PIPE_LIBPLACEBO
+                                                                                                      : h2s::PIPE_CPU);
+  const bool lp = k->pipe == h2s::PIPE_LIBPLACEBO;
+  k->rgba8 = lp && p->lut_enabled ? 1 : 0;
+  k->t_white = isnan(p->target_white) ? (lp ? 203.0 : p->npl) : p->target_white;
+  k->t_black = isnan(p->target_black) ? (lp ? k->t_white / 1000.0 : 0.0) : p->target_black;
+  k->knee_off = isnan(p->knee_offset) ? 1.0 : p->knee_offset;
+  {
+    const double lb = pow(k->t_black / k->t_white, 1.0 / 2.4), a = pow(1.0 - lb, 2.4);
+    k->enc_ainv = (float)(1.0 / a);
+    k->enc_b = (float)(lb / (1.0 - lb));
+  }
+  bt2390_consts(peak, k);
   k->sp_contrast = isnan(p->tm_param) ? 0.5f : (float)p->tm_param;
-  spline_consts(peak, 0.0, p->npl, k->sp_contrast, k);
+  spline_consts(peak, 0.0, k->sp_contrast, k);
   k->npl_1e4 = (float)(p->npl / 10000.0);
-  k->e4_npl = (float)(10000.0 / p->npl);
+  k->e4_npl = (float)(10000.0 / k->t_white);
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
   const double m[9] = {1.6604910021, -0.5876411388, -0.0728498633, -0.1245504745, 1.1328998971,
                        -0.0083494226, -0.0181507634, -0.1005788980, 1.1187296614};
@@ -272,10 +320,14 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   k->k709[0] = (float)r709, k->k709[1] = (float)g709, k->k709[2] = (float)b709;
   k->kcb[0] = (float)(-r709 / 1.8556), k->kcb[1] = (float)(-g709 / 1.8556), k->kcb[2] = (float)(0.9278 / 1.8556);
   k->kcr[0] = (float)(0.7874 / 1.5748), k->kcr[1] = (float)(-g709 / 1.5748), k->kcr[2] = (float)(-b709 / 1.5748);
-  const int q = p->mode == H2S_MODE_NATIVE ? p->bits_out : 8;
+  // quantisation depth (oracle resolve): eq's yuv420p (compat8) or bits_out
+  // (native; the libplacebo rgba frame with gamma 1 has no eq to pass)
+  const int q = p->mode == H2S_MODE_NATIVE || (k->rgba8 && p->gamma == 1.0) ? p->bits_out : 8;
   k->qmax = (1 << q) - 1;
   k->qscale = (float)(1 << (q - 8));
-  k->shift_out = p->mode == H2S_MODE_NATIVE ? 0 : p->bits_out - 8;
+  k->shift_out = p->bits_out - q;
+  k->dither = p->dither == H2S_DITHER_ORDERED && q == 8 ? 1 : 0;
+  k->expand_rep = p->expand == H2S_EXPAND_REPLICATE ? 1 : 0;
   // S7 vf_eq create_lut, generalised to 2^q entries
   const int qn = 1 << q;
   eq->assign(qn, 0);
@@ -472,6 +524,14 @@ void h2s_params_default(h2s_params* p) {
   p->lut_enabled = 1;
   p->mode = H2S_MODE_COMPAT8;
   p->desat_luma = H2S_DESAT_LUMA_RGB;
+  // [EXT] switches: the round-1 models; pipeline AUTO; libplacebo targets from the branch
+  p->chroma_filter = H2S_CHROMA_BOX;
+  p->dither = H2S_DITHER_NONE;
+  p->expand = H2S_EXPAND_SHIFT;
+  p->pipeline = H2S_PIPE_AUTO;
+  p->knee_offset = NAN;
+  p->target_black = NAN;
+  p->target_white = NAN;
 }
 
 int h2s_create(int device, h2s_ctx** out) {
@@ -506,6 +566,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_prev) hipFree(c->d_prev);
   if (c->d_peak) hipFree(c->d_peak);
   if (c->d_curve) hipFree(c->d_curve);
+  if (c->d_chr) hipFree(c->d_chr);
   if (c->curve_ev) hipEventDestroy(c->curve_ev);
   for (int i = 0; i < kEvRing; i++) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
@@ -518,10 +579,21 @@ void h2s_destroy(h2s_ctx* c) {
   delete c;
 }
 
+// set_params / set_lut rewrite device tables that kernels already queued on
+// any stream may still read: drain the device first (include/h2s.h)
+static int drain_launches(h2s_ctx* c) {
+  if (!c->launched) return 0;
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(c, e, "draining queued launches");
+  c->launched = false;
+  return 0;
+}
+
 int h2s_set_lut(h2s_ctx* c, const float* rgb, int n) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (!rgb || n < 2 || n > 256) return fail(c, H2S_E_INVALID_ARG, "LUT size must be in [2, 256]");
   DeviceGuard g(c->device);
+  if (int rc = drain_launches(c)) return rc;
   const size_t cnt = (size_t)n * n * n;
   std::vector<float4> host(cnt);
   for (size_t i = 0; i < cnt; i++) host[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.0f);
@@ -551,6 +623,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   int rc = validate_params(c, p);
   if (rc) return rc;
   DeviceGuard g(c->device);
+  if ((rc = drain_launches(c))) return rc;
   std::vector<uint16_t> eq;
   KParams k;
   resolve(p, &k, &eq);
@@ -585,6 +658,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
 static void curve_fast(const KParams& k, h2s::CurveConsts* cc) {
   cc->b_srcmin = k.b_srcmin, cc->b_range = k.b_range, cc->b_inv_range = k.b_inv_range;
   cc->b_ks = k.b_ks, cc->b_inv_1mks = k.b_inv_1mks, cc->b_maxlum = k.b_maxlum;
+  cc->b_minlum = k.b_minlum, cc->b_bp = k.b_bp, cc->b_gain = k.b_gain;
   cc->sp_srcmin = k.sp_srcmin, cc->sp_srcmax = k.sp_srcmax, cc->sp_kin = k.sp_kin, cc->sp_kout = k.sp_kout;
   cc->sp_pa = k.sp_pa, cc->sp_pb = k.sp_pb, cc->sp_qa = k.sp_qa, cc->sp_qb = k.sp_qb, cc->sp_qc = k.sp_qc;
   cc->sp_dmin = k.sp_dmin, cc->sp_dmax = k.sp_dmax;
@@ -707,12 +781,54 @@ static hipError_t launch_tail(const KParams& k, int nframes, bool vec, bool out8
   return h2s::launch_process(kt, vec, out8, s);
 }
 
+// BICUBIC chroma taps (oracle_chroma_taps): horizontal 7 taps around the
+// left-sited position, vertical 8 around the centre-sited one, normalised
+static void chroma_taps(float* wx7, float* wy8) {
+  auto bic = [](double x) {
+    const double B = 0.0, C = 0.6;
+    x = fabs(x);
+    if (x < 1.0) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) / 6.0;
+    if (x < 2.0) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) / 6.0;
+    return 0.0;
+  };
+  double tx[7], ty[8], sx = 0, sy = 0;
+  for (int i = 0; i < 7; i++) sx += (tx[i] = bic((i - 3) / 2.0));
+  for (int j = 0; j < 8; j++) sy += (ty[j] = bic((j - 3.5) / 2.0));
+  for (int i = 0; i < 7; i++) wx7[i] = (float)(tx[i] / sx);
+  for (int j = 0; j < 8; j++) wy8[j] = (float)(ty[j] / sy);
+}
+
+// BICUBIC chroma: frame by frame, per-pixel chroma into the context scratch
+// then the decimation (h2s_kernels.hip launch_two_pass)
+static hipError_t launch_two_pass_frames(const h2s_ctx* c, const KParams& k, bool out8, int nframes, hipStream_t s) {
+  float wx[7], wy[8];
+  chroma_taps(wx, wy);
+  for (int f = 0; f < nframes; f++) {
+    KParams kf = k;
+    for (int p = 0; p < 3; p++) {
+      kf.in[p] += f * kf.in_fp[p];
+      kf.out[p] += f * kf.out_fp[p];
+    }
+    kf.nframes = 1;
+    kf.total = (long long)kf.ch * kf.ngx;
+    kf.chr444 = c->d_chr;
+    hipError_t e = h2s::launch_two_pass(kf, wx, wy, out8, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 // one launch of the chain over nframes frames described by k.  cvf: per-frame
 // curve records (dynamic peak, fast kernel); tail = false leaves the ragged
-// right columns to the caller
+// right columns to the caller; dbg > 0: the tile kernel's debug instance for
+// that stage, writing frame 0's planes to dbg_out
 static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
-                               hipStream_t s, const h2s::CurveConsts* cvf = nullptr, bool tail = true) {
-  if (!fast) return h2s::launch_process(k, vec, out8, s);
+                               hipStream_t s, const h2s::CurveConsts* cvf = nullptr, bool tail = true, int dbg = 0,
+                               float* dbg_out = nullptr) {
+  if (!fast) {
+    if (c->params.chroma_filter == H2S_CHROMA_BICUBIC) return launch_two_pass_frames(c, k, out8, nframes, s);
+    return h2s::launch_process(k, vec, out8, s);
+  }
   FastParams F;
   resolve_fast(c, k, &F);
   for (int p = 0; p < 3; p++) {
@@ -733,10 +849,53 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
   F.cv_frames = cvf;
+  F.dbg = dbg_out;
+  F.dbg_w = k.W;
+  F.dbg_lut = c->d_lut;
+  F.inv_nm1 = 1.0f / (float)(c->lut_n - 1);
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
-  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, s);
-  if (e != hipSuccess || w64 == k.W || !tail) return e;
+  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, s, dbg);
+  if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
   return launch_tail(k, nframes, vec, out8, s);
+}
+
+// the tile kernel serves: the CPU chain (the libplacebo branch's rgba8 /
+// target / black-point stages run on the generic kernel), the LUT on at
+// N <= 177 (its lattice byte offsets are formed in float32, exact for
+// multiples of 4 below 2^26 = 12 * 177^3 + margin), the default [EXT]
+// switches, 10/12-bit input and BASELINE's operators; frames with a 64-wide
+// tile and 16-byte aligned rows
+static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
+  const h2s_params& p = c->params;
+  if (!c->fast_enabled || !k.lut_enabled || !h2s::fast_supported(k.tonemap)) return false;
+  if (c->lut_n > 177) return false;
+  if (k.pipe != h2s::PIPE_CPU) return false;
+  if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out)) return false;
+  if ((k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE) &&
+      (k.b_minlum != 0.0f || k.t_white != p.npl))
+    return false;  // the folded curve decodes through the npl-scaled EOTF table
+  return true;
+}
+
+static int choose_path(const h2s_ctx* c, const KParams& k, const h2s_frames* din, const h2s_frames* dout,
+                       bool out8) {
+  if (fast_params_ok(c, k) && tile_ok(din, dout, out8))
+    return (din->width & 63) ? H2S_PATH_TILE_TAIL : H2S_PATH_TILE;
+  return c->params.chroma_filter == H2S_CHROMA_BICUBIC ? H2S_PATH_TWO_PASS : H2S_PATH_GENERIC;
+}
+
+static int ensure_chr(h2s_ctx* c, const KParams& k) {
+  const size_t need = (size_t)k.W * k.H;
+  if (need <= c->chr_cap) return 0;
+  if (c->d_chr) hipFree(c->d_chr);
+  c->d_chr = nullptr;
+  c->chr_cap = 0;
+  if (hipMalloc((void**)&c->d_chr, need * sizeof(float2)) != hipSuccess) {
+    c->d_chr = nullptr;
+    return fail(c, H2S_E_OOM, "bicubic chroma scratch allocation failed");
+  }
+  c->chr_cap = need;
+  return 0;
 }
 
 // libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):
@@ -799,8 +958,8 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
     }
     KParams& kf = kfs[f];
     const double peak = peak_update(c, fmax, fsum / npx, k.peak);
-    bt2390_consts(peak, c->params.npl, &kf);
-    spline_consts(peak, c->pk_avg, c->params.npl, k.sp_contrast, &kf);
+    bt2390_consts(peak, &kf);
+    spline_consts(peak, c->pk_avg, k.sp_contrast, &kf);
     if (fast) curve_fast(kf, &c->h_curve[f]);
     for (int p = 0; p < 3; p++) {
       kf.in[p] += f * kf.in_fp[p];
@@ -977,12 +1136,13 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   }
   fill_geometry(&k, &din, &dout, nframes);
   const bool vec = vec_ok(&din, false) && vec_ok(&dout, out8);
-  // fast path: specialised kernel over whole 4-quad groups; the generic
-  // kernel covers unsupported operators, LUT-off, unaligned buffers and the
-  // ragged tail columns (cw % 4)
-  const bool fast = c->fast_enabled && tile_ok(&din, &dout, out8) && k.lut_enabled &&
-                    h2s::fast_supported(k.tonemap);
+  // fast path: the tile kernel over whole 64 x 32 tiles; the generic kernel
+  // covers the rest (choose_path / fast_params_ok) and the ragged columns
+  const int path = choose_path(c, k, &din, &dout, out8);
+  const bool fast = path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL;
   if (fast && (rc = ensure_lut_yuv(c, k, s))) return rc;
+  if (path == H2S_PATH_TWO_PASS && (rc = ensure_chr(c, k))) return rc;
+  c->launched = true;
   const bool dyn_peak = c->params.peak_detect && (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE);
   // the dynamic peak walks frames in order with a host round trip per frame,
   // so it keeps the serial schedule
@@ -1026,7 +1186,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
 int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb, int out_location,
                     void* hip_stream) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
-  if (stage < H2S_STAGE_LINEAR || stage > H2S_STAGE_LUT) return fail(c, H2S_E_INVALID_ARG, "bad stage");
+  if (stage < H2S_STAGE_LINEAR || stage > H2S_STAGE_YUV) return fail(c, H2S_E_INVALID_ARG, "bad stage");
   if (!out_rgb) return fail(c, H2S_E_INVALID_ARG, "out_rgb is NULL");
   KParams k;
   int rc = prepare(c, &k);
@@ -1035,32 +1195,80 @@ int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb,
   DeviceGuard g(c->device);
   hipStream_t s = (hipStream_t)hip_stream;
   const size_t npx = (size_t)in->width * in->height, ob = npx * 3 * sizeof(float);
-  void* din_mem = nullptr;
-  float* dout = out_rgb;
+  // scratch: a tight device copy of the input (host input), the float planes
+  // (host output) and one output frame for the tile kernel's own stores
+  h2s_frames fo{};
+  fo.width = in->width, fo.height = in->height, fo.bits = c->params.bits_out, fo.location = H2S_LOC_DEVICE;
+  const size_t ib = in->location == H2S_LOC_HOST ? (frame_bytes(in) + 255) / 256 * 256 : 0;
+  const size_t fb = (frame_bytes(&fo) + 255) / 256 * 256, pb = out_location == H2S_LOC_HOST ? ob : 0;
+  void* scratch = nullptr;
+  hipError_t e = hipMalloc(&scratch, ib + fb + pb + 256);
+  if (e != hipSuccess) return fail(c, H2S_E_OOM, "debug alloc");
+  uint8_t* base = (uint8_t*)scratch;
   h2s_frames din = *in;
-  hipError_t e;
   if (in->location == H2S_LOC_HOST) {
-    if ((e = hipMalloc(&din_mem, frame_bytes(in))) != hipSuccess) return fail(c, H2S_E_OOM, "debug alloc");
-    din = tight(in, din_mem);
+    din = tight(in, base);
     if ((e = copy_frames(&din, in, 1, s)) != hipSuccess) {
-      hipFree(din_mem);
+      hipFree(scratch);
       return hip_fail(c, e, "debug copy");
     }
   }
-  if (out_location == H2S_LOC_HOST) {
-    if ((e = hipMalloc((void**)&dout, ob)) != hipSuccess) {
-      if (din_mem) hipFree(din_mem);
-      return fail(c, H2S_E_OOM, "debug alloc");
-    }
-  }
-  fill_geometry(&k, &din, nullptr, 1);
+  fo = tight(&fo, base + ib);
+  float* dout = out_location == H2S_LOC_HOST ? (float*)(base + ib + fb) : out_rgb;
+  fill_geometry(&k, &din, &fo, 1);
+  const bool out8 = c->params.bits_out == 8;
+  const int path = choose_path(c, k, &din, &fo, out8);
+  // the generic debug kernel covers every pixel; on the tile path the tile
+  // kernel's debug instance then rewrites the tile columns with its own values
   e = h2s::launch_debug(k, stage, dout, s);
+  if (e == hipSuccess && (path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL)) {
+    if ((rc = ensure_lut_yuv(c, k, s))) {
+      hipStreamSynchronize(s);
+      hipFree(scratch);
+      return rc;
+    }
+    e = launch_chain(c, k, true, false, out8, 1, s, nullptr, false, stage, dout);
+  }
+  c->launched = true;
   if (e == hipSuccess && out_location == H2S_LOC_HOST) e = hipMemcpyAsync(out_rgb, dout, ob, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (din_mem) hipFree(din_mem);
-  if (out_location == H2S_LOC_HOST) hipFree(dout);
+  hipStreamSynchronize(s);
+  hipFree(scratch);
   if (e != hipSuccess) return hip_fail(c, e, "debug kernel");
   return 0;
+}
+
+int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  switch (key) {
+    case H2S_OPT_FAST_PATH:
+      c->fast_enabled = value != 0;
+      return 0;
+    case H2S_OPT_TILES_PER_BLOCK:
+      if (value < 1 || value > 64) return fail(c, H2S_E_INVALID_ARG, "tiles per block must be in [1, 64]");
+      c->tiles_per_block = (int)value;
+      return 0;
+    case H2S_OPT_HOST_SERIAL:
+      c->serial_host = value != 0;
+      return 0;
+    default:
+      return fail(c, H2S_E_INVALID_ARG, "unknown option");
+  }
+}
+
+int h2s_query_path(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  KParams k;
+  int rc = prepare(c, &k);
+  if (rc) return rc;
+  if ((rc = check_frames(c, in, c->params.bits_in, "input"))) return rc;
+  if ((rc = check_frames(c, out, c->params.bits_out, "output"))) return rc;
+  // host sets are staged into tight device copies, whose alignment decides
+  h2s_frames din = *in, dout = *out;
+  uint8_t* fake = (uint8_t*)(uintptr_t)4096;
+  if (in->location == H2S_LOC_HOST) din = tight(in, fake);
+  if (out->location == H2S_LOC_HOST) dout = tight(out, fake);
+  return choose_path(c, k, &din, &dout, c->params.bits_out == 8);
 }
 
 // ---- preview ---------------------------------------------------------------

@@ -42,6 +42,12 @@ struct KParams {
   float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;
   float sp_contrast;
   double peak;            // resolved static source peak (units of 100 nits; host side)
+  // libplacebo bt2390 black-point adaptation (min_lum = 0: off)
+  float b_minlum, b_bp, b_gain;
+  double t_black, t_white, knee_off;  // SDR target (nits) and BT.2390 knee offset (host side)
+  // pipeline (h2s_pipeline, resolved to CPU_CHAIN or LIBPLACEBO)
+  int pipe, rgba8;
+  float enc_ainv, enc_b;  // libplacebo BT.1886 encode: (x * ainv)^(1/2.4) - b
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
   float lut_max;
@@ -52,16 +58,22 @@ struct KParams {
   float qscale;
   int eq_identity;
   const uint16_t* eq_lut;
+  int dither;             // ordered 8x8 dither at the 8-bit quantiser
+  int expand_rep;         // S8 bit replication instead of a shift
   // Y'CbCr 709 rows
   float k709[3], kcb[3], kcr[3];
   int gx0;  // first column group this launch covers (tail launches)
+  float2* chr444;         // BICUBIC: per-pixel (Cb, Cr) of one frame (two-pass path)
 };
+
+constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
 
 // Constants of the PQ-domain curves (BT.2390 / spline) in the fast kernel's
 // folded form.  They are the only parameters that change from frame to frame
 // under dynamic peak detection, so a launch can take one record per frame.
 struct CurveConsts {
   float b_srcmin, b_range, b_inv_range, b_ks, b_inv_1mks, b_maxlum;  // BT.2390, HLG input
+  float b_minlum, b_bp, b_gain;  // black-point adaptation (b_minlum = 0: off)
   // PQ-input forms that land directly on pq_z's table coordinate u = e*PQ_SEG + 1:
   // BT.2390: e1n = med3(e1*e1a + e1b), t = e1n*ta + tb, u = c3..c0 Horner (knee) or e1n*lr + lc
   float b_e1a, b_e1b, b_ta, b_tb, b_c3, b_c2, b_c1, b_c0, b_lr, b_lc, b_thr;
@@ -110,6 +122,12 @@ struct FastParams : CurveConsts {
   // S1 PQ EOTF (x 10000/npl) as a piecewise cubic: segment i covers
   // E in [i, i+1)/PQ_SEG, coefficients (c3, c2, c1, c0) of t = E*PQ_SEG - i
   const float4* pq_tab;
+  // debug instances (k_tile<..., DBG>): stage planes of frame 0, row pitch
+  // dbg_w floats; the float4 RGB lattice for stage 4; 1 / (N-1)
+  float* dbg;
+  int dbg_w;
+  const float4* dbg_lut;
+  float inv_nm1;
 };
 
 constexpr int PQ_SEG = 128;          // segments per unit of E
@@ -175,6 +193,16 @@ __device__ __forceinline__ float spline_pq(const K& P, float e) {
   return fminf(fmaxf(y + P.sp_kout, P.sp_dmin), P.sp_dmax);
 }
 
+// libplacebo bt2390 black-point adaptation on the normalised curve output
+// (x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum, for x < 1)
+__device__ __forceinline__ float bt2390_black(float mn, float bp, float gain, float x) {
+  if (!(mn > 0.0f) || !(x < 1.0f)) return x;
+  const float om = 1.0f - x;
+  const float pw = bp == 4.0f ? (om * om) * (om * om) : fpow(om, bp);
+  x += mn * pw;
+  return gain * (x - mn) + mn;
+}
+
 // S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)
 __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g, float& b) {
   float sig, sig_orig;
@@ -196,6 +224,7 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
       e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * P.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - P.b_ks) +
            (-2.0f * t3 + 3.0f * t2) * P.b_maxlum;
     }
+    e2 = bt2390_black(P.b_minlum, P.b_bp, P.b_gain, e2);
     float s2 = pq_eotf(e2 * P.b_range + P.b_srcmin) * P.e4_npl;
     float k = s2 * frcp(sig);
     r *= k, g *= k, b *= k;
@@ -282,6 +311,29 @@ __device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g
   b = w0 * c000.z + w1 * c1.z + w2 * c2.z + w3 * c111.z;
 }
 
+// libplacebo branch: BT.1886 encode against the target black (oracle lp_encode)
+__device__ __forceinline__ float lp_encode(const KParams& P, float x) {
+  x = x > 0.0f ? x : 0.0f;
+  return fpow(x * P.enc_ainv, 1.0f / 2.4f) - P.enc_b;
+}
+
+// libplacebo branch: rgba8 download (round to nearest), then vf_lut3d's 8-bit
+// path: coordinate clip((q / 255) (N-1)), tetrahedral, output truncated to
+// 8 bits; returns the 8-bit values / 255
+__device__ __forceinline__ float rgba8_q(float v) { return floorf(clamp01(v) * 255.0f + 0.5f); }
+
+__device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g, float& b);
+__device__ __forceinline__ void lut3d_8bit(const KParams& P, float& r, float& g, float& b) {
+  const float sf = 1.0f / 255.0f;
+  // lut3d_tetra multiplies by lut_max and clips; (q * 1/255) is its input
+  r = rgba8_q(r) * sf, g = rgba8_q(g) * sf, b = rgba8_q(b) * sf;
+  lut3d_tetra(P, r, g, b);
+  const float R = fminf(fmaxf(truncf(r * 255.0f), 0.0f), 255.0f);
+  const float G = fminf(fmaxf(truncf(g * 255.0f), 0.0f), 255.0f);
+  const float B = fminf(fmaxf(truncf(b * 255.0f), 0.0f), 255.0f);
+  r = R * sf, g = G * sf, b = B * sf;
+}
+
 // S1 (after upsampling) .. S4 on one pixel.  UPTO = last stage to apply.
 template <int UPTO>
 __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, float cr, float& r, float& g,
@@ -302,6 +354,19 @@ __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, fl
   if (UPTO == 1) return;
   tonemap_px(P, r, g, b);
   if (UPTO == 2) return;
+  if (P.pipe == PIPE_LIBPLACEBO) {
+    if (P.lut_enabled) {
+      r = lp_encode(P, r), g = lp_encode(P, g), b = lp_encode(P, b);
+      if (UPTO == 3) return;
+      lut3d_8bit(P, r, g, b);
+    } else {
+      float mr = P.m709[0] * r + P.m709[1] * g + P.m709[2] * b;
+      float mg = P.m709[3] * r + P.m709[4] * g + P.m709[5] * b;
+      float mb = P.m709[6] * r + P.m709[7] * g + P.m709[8] * b;
+      r = clamp01(lp_encode(P, mr)), g = clamp01(lp_encode(P, mg)), b = clamp01(lp_encode(P, mb));
+    }
+    return;
+  }
   if (P.lut_enabled) {
     r = bt1886_inv(r), g = bt1886_inv(g), b = bt1886_inv(b);
     if (UPTO == 3) return;
@@ -317,6 +382,27 @@ __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, fl
 __device__ __forceinline__ int quant(float v, int qmax) {
   int i = (int)floorf(v + 0.5f);
   return min(max(i, 0), qmax);
+}
+
+// swscale ff_dither_8x8_128 (1/128 LSB): the H2S_DITHER_ORDERED rounding
+__device__ __forceinline__ float dither_off(int x, int y) {
+  constexpr unsigned char T[8][8] = {
+      {36, 68, 60, 92, 34, 66, 58, 90},   {100, 4, 124, 28, 98, 2, 122, 26},
+      {52, 84, 44, 76, 50, 82, 42, 74},   {116, 20, 108, 12, 114, 18, 106, 10},
+      {32, 64, 56, 88, 38, 70, 62, 94},   {96, 0, 120, 24, 102, 6, 126, 30},
+      {48, 80, 40, 72, 54, 86, 46, 78},   {112, 16, 104, 8, 118, 22, 110, 14}};
+  return (float)T[y & 7][x & 7] * (1.0f / 128.0f);
+}
+
+__device__ __forceinline__ int quant_o(float v, float off, int qmax) {
+  int i = (int)floorf(v + off);
+  return min(max(i, 0), qmax);
+}
+
+// S8 expansion of a quantised code to the output depth
+__device__ __forceinline__ int expand_code(const KParams& P, int v) {
+  if (!P.shift_out) return v;
+  return P.expand_rep ? (v << P.shift_out) | (v >> (8 - P.shift_out)) : v << P.shift_out;
 }
 
 }  // namespace h2s

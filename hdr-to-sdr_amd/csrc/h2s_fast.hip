@@ -351,7 +351,11 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 // are issued before tile i is computed, so after the first tile the block no
 // longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
 // barrier, 8 compute steps, barrier, store, barrier.
-template <int TRC, int TM, int DESAT>
+// DBG (debug instances only, never launched by h2s_process): 1..5 = also
+// write that h2s_stage's three float planes for frame 0 to F.dbg (W x H each)
+// from this kernel's own arithmetic — stage 4 blends the float4 RGB lattice
+// F.dbg_lut with the same cell, corners and weights as the Y'CbCr lattice
+template <int TRC, int TM, int DESAT, int DBG = 0>
 // 5 waves per SIMD = the LDS-bound occupancy (5 blocks of ~27.6 KB per CU;
 // 3 and 6 measured slower): let the compiler use the VGPRs that allows
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
@@ -463,7 +467,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const float eb = fmaf(U, a_bu, ybs);
       float r, gg, bl;
       const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
+      // debug: this step's pixel in frame 0 (plane index), -1 = not written
+      const long long di = DBG && g.f == 0 && g.py0 + yl + 8 * (s >> 1) < F.H
+                               ? (long long)(g.py0 + yl + 8 * (s >> 1)) * F.dbg_w + g.px0 + xl + 8 * (s & 1)
+                               : -1;
+      const long long dpl = (long long)F.dbg_w * F.H;
+      auto dput = [&](float a, float b_, float c) {
+        if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
+      };
+      if (DBG == 1) dput(r, gg, bl);
       tone<TRC, TM, DESAT>(F, cv, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
+      if (DBG == 2) dput(r, gg, bl);
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
       const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
@@ -483,6 +497,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
       const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
       const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+      if (DBG == 3) dput(sr * F.inv_nm1, sg * F.inv_nm1, sb * F.inv_nm1);
+      if (DBG == 4) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
+        const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
+                     q3 = F.dbg_lut[(base + F.c111) / 12];
+        dput(w0 * q0.x + w1 * q1.x + w2 * q2.x + w3 * q3.x, w0 * q0.y + w1 * q1.y + w2 * q2.y + w3 * q3.y,
+             w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
+      }
+      if (DBG == 5) dput(o.x - 0.5f, 4.0f * o.y, 4.0f * o.z);
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
       // chroma: 2x2 sums; the 4 lanes of a quad store the same value
@@ -583,19 +605,26 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
-// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma
-hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s) {
+// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma.  dbg: 0 = the
+// product kernel; 1..5 = its debug instance for that h2s_stage (F.dbg set)
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s, int dbg) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
   if (nt == 0) return hipSuccess;
   const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb), block(256);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8) desat = 0;
-#define K_FAST k_tile
-#define X(T, M, D)                                                   \
-  if (trc == T && tm == M && desat == D) {                           \
-    hipLaunchKernelGGL((K_FAST<T, M, D>), grid, block, lds, s, F);   \
-    return hipGetLastError();                                        \
+#define X(T, M, D)                                                                        \
+  if (trc == T && tm == M && desat == D) {                                                \
+    switch (dbg) {                                                                        \
+      case 0: hipLaunchKernelGGL((k_tile<T, M, D, 0>), grid, block, lds, s, F); break;    \
+      case 1: hipLaunchKernelGGL((k_tile<T, M, D, 1>), grid, block, lds, s, F); break;    \
+      case 2: hipLaunchKernelGGL((k_tile<T, M, D, 2>), grid, block, lds, s, F); break;    \
+      case 3: hipLaunchKernelGGL((k_tile<T, M, D, 3>), grid, block, lds, s, F); break;    \
+      case 4: hipLaunchKernelGGL((k_tile<T, M, D, 4>), grid, block, lds, s, F); break;    \
+      default: hipLaunchKernelGGL((k_tile<T, M, D, 5>), grid, block, lds, s, F); break;   \
+    }                                                                                     \
+    return hipGetLastError();                                                             \
   }
   FAST_CASES(X)
 #undef X

@@ -31,7 +31,10 @@ __device__ __forceinline__ int ld16(const uint8_t* row, int x) {
   return *reinterpret_cast<const uint16_t*>(row + 2 * x);
 }
 
-template <int QPT, bool VEC, bool OUT8>
+// C444: BICUBIC chroma (two-pass path): store every pixel's (Cb, Cr) into
+// P.chr444 (frame 0 of the launch, W x H) instead of the 2x2 mean; the
+// chroma planes are then written by k_chroma_bicubic
+template <int QPT, bool VEC, bool OUT8, bool C444 = false>
 __global__ __launch_bounds__(256) void k_process(const KParams P) {
   const long long lb = xcd_remap(blockIdx.x, gridDim.x);
   const long long item = lb * 256 + threadIdx.x;
@@ -123,14 +126,18 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
       const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
       cbs[p] = P.kcb[0] * r + P.kcb[1] * g + P.kcb[2] * b;
       crs[p] = P.kcr[0] * r + P.kcr[1] * g + P.kcr[2] * b;
-      int yq = quant((16.0f + 219.0f * Y) * P.qscale, P.qmax);
+      const int px = 2 * (cx0 + k) + (p & 1), py = 2 * cy + j;
+      int yq = quant_o((16.0f + 219.0f * Y) * P.qscale, P.dither ? dither_off(px, py) : 0.5f, P.qmax);
       if (!P.eq_identity) yq = P.eq_lut[yq];
-      yo[j][x] = yq << P.shift_out;
+      yo[j][x] = expand_code(P, yq);
+      if (C444 && px < P.W) P.chr444[(long long)py * P.W + px] = make_float2(cbs[p], crs[p]);
     }
+    if (C444) continue;
     const float cb = ((cbs[0] + cbs[1]) + (cbs[2] + cbs[3])) * 0.25f;
     const float cr = ((crs[0] + crs[1]) + (crs[2] + crs[3])) * 0.25f;
-    uo[k] = quant((128.0f + 224.0f * cb) * P.qscale, P.qmax) << P.shift_out;
-    vo[k] = quant((128.0f + 224.0f * cr) * P.qscale, P.qmax) << P.shift_out;
+    const float co = P.dither ? dither_off(cx0 + k, cy) : 0.5f;
+    uo[k] = expand_code(P, quant_o((128.0f + 224.0f * cb) * P.qscale, co, P.qmax));
+    vo[k] = expand_code(P, quant_o((128.0f + 224.0f * cr) * P.qscale, co, P.qmax));
   }
 
   // ---- stores ----
@@ -161,6 +168,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
       }
     }
   }
+  if (C444) return;
   uint8_t* ru = P.out[1] + f * P.out_fp[1] + cy * P.out_ls[1];
   uint8_t* rv = P.out[2] + f * P.out_fp[2] + cy * P.out_ls[2];
   if (VEC && full && QPT == 4) {
@@ -219,10 +227,56 @@ __global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
   const float cb = up(1), cr = up(2);
   const float yv = (float)ld16(P.in[0] + y * P.in_ls[0], x) * P.y_scale + P.y_off;
   float r, g, b;
-  chain_px<STAGE>(P, yv, cb, cr, r, g, b);
+  chain_px<STAGE < 5 ? STAGE : 4>(P, yv, cb, cr, r, g, b);
+  if (STAGE == 5) {  // S6 quantiser inputs (oracle px_yuv)
+    r = clamp01(r), g = clamp01(g), b = clamp01(b);
+    const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
+    const float cbp = P.kcb[0] * r + P.kcb[1] * g + P.kcb[2] * b;
+    const float crp = P.kcr[0] * r + P.kcr[1] * g + P.kcr[2] * b;
+    r = (16.0f + 219.0f * Y) * P.qscale, g = 224.0f * P.qscale * cbp, b = 224.0f * P.qscale * crp;
+  }
   out[i] = r;
   out[npx + i] = g;
   out[2 * npx + i] = b;
+}
+
+// BICUBIC chroma decimation (second pass): one thread per output chroma
+// sample of one frame; separable taps (oracle process_frame_bicubic order:
+// horizontal 7-tap sums per luma row, then the vertical 8-tap sum)
+struct ChromaTaps {
+  float wx[7], wy[8];
+};
+
+template <bool OUT8>
+__global__ __launch_bounds__(256) void k_chroma_bicubic(const KParams P, const ChromaTaps T) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P.cw * P.ch) return;
+  const int k = i % P.cw, m = i / P.cw;
+  float su = 0.0f, sv = 0.0f;
+  for (int j = 0; j < 8; j++) {
+    const int y = min(max(2 * m - 3 + j, 0), P.H - 1);
+    const float2* row = P.chr444 + (long long)y * P.W;
+    float hu = 0.0f, hv = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 7; t++) {
+      const float2 c = row[min(max(2 * k - 3 + t, 0), P.W - 1)];
+      hu += T.wx[t] * c.x;
+      hv += T.wx[t] * c.y;
+    }
+    su += T.wy[j] * hu;
+    sv += T.wy[j] * hv;
+  }
+  const float co = P.dither ? dither_off(k, m) : 0.5f;
+  const int u = expand_code(P, quant_o((128.0f + 224.0f * su) * P.qscale, co, P.qmax));
+  const int v = expand_code(P, quant_o((128.0f + 224.0f * sv) * P.qscale, co, P.qmax));
+  uint8_t* ru = P.out[1] + m * P.out_ls[1];
+  uint8_t* rv = P.out[2] + m * P.out_ls[2];
+  if (OUT8) {
+    ru[k] = (uint8_t)u, rv[k] = (uint8_t)v;
+  } else {
+    reinterpret_cast<uint16_t*>(ru)[k] = (uint16_t)u;
+    reinterpret_cast<uint16_t*>(rv)[k] = (uint16_t)v;
+  }
 }
 
 // ---- host-side launchers (called from h2s_api.hip) ----------------------
@@ -248,8 +302,26 @@ hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s) 
     case 1: hipLaunchKernelGGL((k_debug<1>), grid, block, 0, s, P, out); break;
     case 2: hipLaunchKernelGGL((k_debug<2>), grid, block, 0, s, P, out); break;
     case 3: hipLaunchKernelGGL((k_debug<3>), grid, block, 0, s, P, out); break;
-    default: hipLaunchKernelGGL((k_debug<4>), grid, block, 0, s, P, out); break;
+    case 4: hipLaunchKernelGGL((k_debug<4>), grid, block, 0, s, P, out); break;
+    default: hipLaunchKernelGGL((k_debug<5>), grid, block, 0, s, P, out); break;
   }
+  return hipGetLastError();
+}
+
+// BICUBIC chroma, one frame (P: nframes 1, in/out at that frame, chr444 set):
+// pass 1 = k_process<C444> (luma + per-pixel chroma), pass 2 = decimation
+hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s) {
+  constexpr int QPT = 4;
+  const long long nb = (P.total + 255) / 256;
+  if (nb == 0) return hipSuccess;
+  if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  else hipLaunchKernelGGL((k_process<QPT, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  ChromaTaps T;
+  for (int i = 0; i < 7; i++) T.wx[i] = wx7[i];
+  for (int j = 0; j < 8; j++) T.wy[j] = wy8[j];
+  const unsigned nc = (unsigned)(((long long)P.cw * P.ch + 255) / 256);
+  if (out8) hipLaunchKernelGGL((k_chroma_bicubic<true>), dim3(nc), dim3(256), 0, s, P, T);
+  else hipLaunchKernelGGL((k_chroma_bicubic<false>), dim3(nc), dim3(256), 0, s, P, T);
   return hipGetLastError();
 }
 

@@ -27,7 +27,14 @@ TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS, TM_BT23
 MODE_COMPAT8, MODE_NATIVE = 0, 1
 DESAT_LUMA_RGB, DESAT_LUMA_BT2020, DESAT_LUMA_BT709 = 0, 1, 2
 LOC_DEVICE, LOC_HOST = 0, 1
-STAGE_LINEAR, STAGE_TONEMAP, STAGE_GAMMA, STAGE_LUT = 1, 2, 3, 4
+STAGE_LINEAR, STAGE_TONEMAP, STAGE_GAMMA, STAGE_LUT, STAGE_YUV = 1, 2, 3, 4, 5
+CHROMA_BOX, CHROMA_BICUBIC = 0, 1
+DITHER_NONE, DITHER_ORDERED = 0, 1
+EXPAND_SHIFT, EXPAND_REPLICATE = 0, 1
+PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
+OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
+PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
+ABI_VERSION = 2
 
 # every symbol include/h2s.h declares (checked by tests/test_abi_exports.py)
 EXPORTS = (
@@ -35,7 +42,7 @@ EXPORTS = (
     'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
     'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
     'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_peak_reset',
-    'h2s_peak_state',
+    'h2s_peak_state', 'h2s_set_option', 'h2s_query_path',
 )
 
 
@@ -56,6 +63,13 @@ class H2SParams(ctypes.Structure):
         ('mode', ctypes.c_int32),
         ('desat_luma', ctypes.c_int32),
         ('peak_detect', ctypes.c_int32),
+        ('chroma_filter', ctypes.c_int32),
+        ('dither', ctypes.c_int32),
+        ('expand', ctypes.c_int32),
+        ('pipeline', ctypes.c_int32),
+        ('knee_offset', ctypes.c_double),
+        ('target_black', ctypes.c_double),
+        ('target_white', ctypes.c_double),
         ('reserved', ctypes.c_int32 * 4),
     ]
 
@@ -138,6 +152,8 @@ def lib() -> ctypes.CDLL:
         'h2s_peak_reset': (ctypes.c_int, [c_ctx]),
         'h2s_peak_state': (ctypes.c_int, [c_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+        'h2s_set_option': (ctypes.c_int, [c_ctx, ctypes.c_int, ctypes.c_int64]),
+        'h2s_query_path': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.POINTER(H2SFrames)]),
         'h2s_preview_size': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
         'h2s_preview_rgb24': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_void_p, ctypes.c_int64,
@@ -148,8 +164,8 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.h2s_abi_version() != 1:
-        raise ImportError(f'libh2s ABI {L.h2s_abi_version()} != 1')
+    if L.h2s_abi_version() != ABI_VERSION:
+        raise ImportError(f'libh2s ABI {L.h2s_abi_version()} != {ABI_VERSION}')
     _lib = L
     return L
 

@@ -51,6 +51,13 @@ _TRC_NAMES = {'smpte2084': _abi.TRC_PQ, 'pq': _abi.TRC_PQ,
 _MODES = {'compat8': _abi.MODE_COMPAT8, 'native': _abi.MODE_NATIVE}
 _DESAT_LUMA = {'rgb': _abi.DESAT_LUMA_RGB, 'bt2020': _abi.DESAT_LUMA_BT2020,
                'bt709': _abi.DESAT_LUMA_BT709}
+# [EXT] switches (include/h2s.h)
+_CHROMA = {'box': _abi.CHROMA_BOX, 'bicubic': _abi.CHROMA_BICUBIC}
+_DITHER = {'none': _abi.DITHER_NONE, 'ordered': _abi.DITHER_ORDERED}
+_EXPAND = {'shift': _abi.EXPAND_SHIFT, 'replicate': _abi.EXPAND_REPLICATE}
+# which of the reference's two chains: 'auto' = libplacebo for the GPU-only
+# operators (the only chain that has them), the CPU chain otherwise
+_PIPELINE = {'auto': _abi.PIPE_AUTO, 'cpu': _abi.PIPE_CPU_CHAIN, 'libplacebo': _abi.PIPE_LIBPLACEBO}
 
 
 def is_gpu_only_tonemapper(tonemapper: str) -> bool:
@@ -80,6 +87,13 @@ class TonemapParams:
     mastering_max: float = 0.0
     desat_luma: str = 'rgb'
     peak_detect: bool = False   # BT.2390 / spline: detected, smoothed per-frame peak (libplacebo peak_detect=1)
+    chroma_filter: str = 'box'  # S6 4:4:4 -> 4:2:0 ('box' | 'bicubic')
+    dither: str = 'none'        # 8-bit quantiser ('none' | 'ordered')
+    expand: str = 'shift'       # S8 8-bit -> bits_out ('shift' | 'replicate')
+    pipeline: str = 'auto'      # 'cpu' (FFMPEG_CONVERT_FILTER) | 'libplacebo' (build_libplacebo_filter) | 'auto'
+    knee_offset: float = math.nan   # BT.2390 knee offset (NaN: libplacebo's 1.0; 0.5 = ITU-R BT.2390)
+    target_black: float = math.nan  # SDR target black, nits (NaN: pipeline default)
+    target_white: float = math.nan  # SDR target white, nits (NaN: libplacebo 203, CPU chain npl)
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
@@ -91,6 +105,13 @@ class TonemapParams:
             raise ValueError(f'unknown mode {self.mode!r}')
         if self.desat_luma not in _DESAT_LUMA:
             raise ValueError(f'unknown desat_luma {self.desat_luma!r}')
+        for name, table in (('chroma_filter', _CHROMA), ('dither', _DITHER), ('expand', _EXPAND),
+                            ('pipeline', _PIPELINE)):
+            if getattr(self, name) not in table:
+                raise ValueError(f'unknown {name} {getattr(self, name)!r}; expected one of {sorted(table)}')
+        if self.pipeline == 'libplacebo' and tm not in GPU_ONLY_TONEMAPPERS:
+            # libplacebo's own hable/mobius/reinhard curves are not restated
+            raise ValueError(f'libplacebo tonemapping={tm} is not supported (only bt.2390 / spline)')
         if self.bits_in not in (10, 12):
             raise ValueError(f'bits_in must be 10 or 12, got {self.bits_in}')
         if self.bits_out not in (8, 10, 12):
@@ -141,7 +162,20 @@ class TonemapParams:
         p.mode = _MODES[self.mode]
         p.desat_luma = _DESAT_LUMA[self.desat_luma]
         p.peak_detect = 1 if self.peak_detect else 0
+        p.chroma_filter = _CHROMA[self.chroma_filter]
+        p.dither = _DITHER[self.dither]
+        p.expand = _EXPAND[self.expand]
+        p.pipeline = _PIPELINE[self.pipeline]
+        p.knee_offset = self.knee_offset
+        p.target_black = self.target_black
+        p.target_white = self.target_white
         return p
+
+    def resolved_pipeline(self) -> str:
+        """'cpu' or 'libplacebo' after 'auto' resolution."""
+        if self.pipeline != 'auto':
+            return self.pipeline
+        return 'libplacebo' if is_gpu_only_tonemapper(self.tonemapper) else 'cpu'
 
     # ---- back to the reference's chain string --------------------------
     def filter_string(self, lut_path: str = '<LUT>') -> str:
@@ -231,14 +265,21 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             kw['lut_enabled'] = True
         elif name == 'libplacebo':
             # GPU chain build_libplacebo_filter (src/utils.py:392-471): the
-            # tone map runs here natively; libplacebo's own gamut/desat
-            # handling is replaced by the lut3d stage that follows it.
+            # tone map runs here natively (the libplacebo pipeline: its
+            # SDR target, BT.1886 encode, rgba8 download, lut3d 8-bit path).
             tm = kv.get('tonemapping')
             if tm is None:
                 raise ValueError('libplacebo stage without tonemapping=')
+            if not is_gpu_only_tonemapper(tm):
+                # the reference emits libplacebo chains for every operator
+                # with use_gpu (src/ffmpeg_command.py:119, :236); libplacebo's
+                # own hable/mobius/reinhard curves differ from vf_tonemap's
+                # and are not restated: refuse rather than mis-map them
+                raise ValueError(f'libplacebo tonemapping={tm} is not supported (only bt.2390 / spline)')
             seen_linear = True
             kw['tonemapper'] = tm.lower()
             kw['desat'] = 0.0
+            kw['pipeline'] = 'libplacebo'
             # peak_detect=1 (src/utils.py:448): per-frame detected, temporally
             # smoothed source peak; libh2s restates it for BT.2390 and spline
             kw['peak_detect'] = kv.get('peak_detect', '0') in ('1', 'true')

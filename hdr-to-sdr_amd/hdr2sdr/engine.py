@@ -126,8 +126,23 @@ class Tonemapper:
         self.process(src, dst, stream)
         return dst
 
+    def set_option(self, key: int, value: int) -> None:
+        """h2s_set_option (_abi.OPT_FAST_PATH / OPT_TILES_PER_BLOCK / OPT_HOST_SERIAL)."""
+        self._check(self._L.h2s_set_option(self._ctx, int(key), int(value)))
+
+    def query_path(self, src: FrameBatch, dst: FrameBatch) -> int:
+        """The kernel path (_abi.PATH_*) h2s_process would take for src -> dst."""
+        di, do = src.descriptor(), dst.descriptor()
+        rc = self._L.h2s_query_path(self._ctx, ctypes.byref(di), ctypes.byref(do))
+        if rc < 0:
+            self._check(rc)
+        return rc
+
     def debug_float(self, src: FrameBatch, stage: int) -> np.ndarray:
-        """float32 [3, H, W] RGB of frame 0 after ``stage`` (1..4)."""
+        """float32 [3, H, W] of frame 0 after ``stage``: R, G, B for 1..4,
+        the quantiser inputs (Y code, Cb, Cr in code units) for 5; computed by
+        the kernel h2s_process would use (the tile kernel's debug instance on
+        the tile path)."""
         out = np.empty((3, src.height, src.width), dtype=np.float32)
         d = src.descriptor()
         self._check(self._L.h2s_debug_float(self._ctx, ctypes.byref(d), int(stage), out.ctypes.data,

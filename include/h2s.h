@@ -19,7 +19,9 @@
  * be used by two threads at once (one context per worker / GPU), and contexts
  * share no mutable global state.  h2s_process is asynchronous on the stream
  * it is given when both frame sets live in device memory; the caller
- * synchronises.
+ * synchronises.  h2s_set_params and h2s_set_lut first wait for every launch
+ * the context has queued (on any stream) to finish, so replacing the tables a
+ * kernel in flight reads is safe.
  *
  * Errors: 0 on success, a negative H2S_E_* code otherwise; the message is
  * available from h2s_last_error(ctx) (or h2s_last_error(NULL) for failures
@@ -37,7 +39,7 @@
 extern "C" {
 #endif
 
-#define H2S_ABI_VERSION 1
+#define H2S_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define H2S_OK 0
@@ -89,12 +91,60 @@ enum h2s_desat_luma {
 /* Where a frame set lives. */
 enum h2s_location { H2S_LOC_DEVICE = 0, H2S_LOC_HOST = 1 };
 
-/* Debug stages for h2s_debug_float (float RGB after each chain stage). */
+/* Debug stages for h2s_debug_float: three float planes per pixel.
+ * 1..4: R, G, B after the stage.  5: the quantiser's inputs, before rounding:
+ * plane 0 = luma code (16 + 219 Y) * 2^(q-8), planes 1/2 = the pixel's Cb / Cr
+ * in code units, 224 * 2^(q-8) * C (the 4:2:0 sample is 128 * 2^(q-8) plus
+ * the chroma filter over these), q = the quantisation depth. */
 enum h2s_stage {
   H2S_STAGE_LINEAR = 1,   /* after S1 zscale=t=linear:npl=100          */
   H2S_STAGE_TONEMAP = 2,  /* after S2 tonemap=                          */
   H2S_STAGE_GAMMA = 3,    /* after S3 zscale=t=bt709 (BT.1886 inverse)  */
-  H2S_STAGE_LUT = 4       /* after S4 lut3d=interp=tetrahedral          */
+  H2S_STAGE_LUT = 4,      /* after S4 lut3d=interp=tetrahedral          */
+  H2S_STAGE_YUV = 5       /* S6 quantiser inputs (see above)            */
+};
+
+/* S6 chroma 4:4:4 -> 4:2:0 filter of the implicit swscale conversion
+ * (cannot be pinned without the bundled ffmpeg).
+ * BOX: the 2x2 mean of the quad (centre siting).  BICUBIC: swscale's default
+ * bicubic (B = 0, C = 0.6) decimation, chroma sited left horizontally (on the
+ * even luma column) and centred vertically, edge-clamped. */
+enum h2s_chroma_filter { H2S_CHROMA_BOX = 0, H2S_CHROMA_BICUBIC = 1 };
+
+/* Rounding of the 8-bit quantiser (S6 yuv420p, or the libplacebo branch's
+ * rgba download).  NONE: round half up.  ORDERED: swscale's 8x8 ordered
+ * dither offsets (ff_dither_8x8_128 / 128 of an LSB) instead of +0.5. */
+enum h2s_dither { H2S_DITHER_NONE = 0, H2S_DITHER_ORDERED = 1 };
+
+/* S8 8-bit -> bits_out expansion after eq. */
+enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
+
+/* Which of the reference's two chains the parameters describe.
+ * CPU_CHAIN: FFMPEG_CONVERT_FILTER (src/utils.py:38-42): zscale -> tonemap ->
+ *   zscale -> lut3d (float) -> yuv420p -> eq -> -pix_fmt.
+ * LIBPLACEBO: build_libplacebo_filter (src/utils.py:392-471) with the LUT on:
+ *   libplacebo tone map (BT.2390 / spline) -> BT.1886 encode against the SDR
+ *   target -> 8-bit rgba download -> lut3d's 8-bit path (truncating output) ->
+ *   Y'CbCr at the output depth (gamma = 1; the chain has no eq) or, with
+ *   eq=gamma, yuv420p -> eq -> -pix_fmt.  With the LUT off the branch keeps
+ *   libplacebo's own BT.709 conversion and nv12 (8-bit) download.
+ * AUTO: LIBPLACEBO for BT2390 / SPLINE (the reference's GPU-only operators
+ *   exist only there), CPU_CHAIN otherwise. */
+enum h2s_pipeline { H2S_PIPE_AUTO = 0, H2S_PIPE_CPU_CHAIN = 1, H2S_PIPE_LIBPLACEBO = 2 };
+
+/* Context options (h2s_set_option). */
+enum h2s_option {
+  H2S_OPT_FAST_PATH = 1,       /* 1 (default): the tile kernel where it applies; 0: generic kernel only */
+  H2S_OPT_TILES_PER_BLOCK = 2, /* tile kernel: 64x32 tiles one block walks (1..64, default 8)          */
+  H2S_OPT_HOST_SERIAL = 3      /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
+};
+
+/* Kernel path h2s_process takes for a given frame pair (h2s_query_path). */
+enum h2s_path {
+  H2S_PATH_TILE = 1,       /* k_tile only (width % 64 == 0)                      */
+  H2S_PATH_TILE_TAIL = 2,  /* k_tile + k_process on the width % 64 columns       */
+  H2S_PATH_GENERIC = 3,    /* k_process                                          */
+  H2S_PATH_TWO_PASS = 4    /* k_process per-pixel chroma + bicubic decimation    */
 };
 
 /* ---- parameters ---------------------------------------------------------
@@ -121,6 +171,20 @@ typedef struct h2s_params {
                          * temporally smoothed source peak (and, for SPLINE,
                          * average: the knee) (libplacebo peak_detect=1,
                          * src/utils.py:448); state lives in the context   */
+  /* [EXT] switches the bundled ffmpeg would settle */
+  int32_t chroma_filter; /* enum h2s_chroma_filter (S6)                     */
+  int32_t dither;        /* enum h2s_dither (8-bit quantiser)               */
+  int32_t expand;        /* enum h2s_expand (S8)                            */
+  int32_t pipeline;      /* enum h2s_pipeline                               */
+  /* libplacebo branch (BT.2390 / SPLINE); NaN = that branch's default      */
+  double knee_offset;    /* BT.2390 knee offset: ks = (1+o) maxLum - o;
+                          * libplacebo default 1.0, ITU-R BT.2390 0.5      */
+  double target_black;   /* SDR target black (nits); NaN: LIBPLACEBO =
+                          * white / 1000 (libplacebo's SDR contrast),
+                          * CPU_CHAIN = 0 (no black-point adaptation)      */
+  double target_white;   /* SDR target white (nits); NaN: LIBPLACEBO = 203
+                          * (libplacebo's SDR white, BT.2408), CPU_CHAIN =
+                          * npl                                            */
   int32_t reserved[4];
 } h2s_params;
 
@@ -173,11 +237,21 @@ int h2s_set_params(h2s_ctx *ctx, const h2s_params *p);
 int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
                 int nframes, void *hip_stream);
 
-/* Debug/parity: float RGB (planar, 3*w*h floats: R plane, G plane, B plane)
- * of frame 0 after `stage` (enum h2s_stage), written to out_rgb (host or
- * device per out_location).  Synchronous. */
+/* Debug/parity: three float planes (3*w*h floats) of frame 0 after `stage`
+ * (enum h2s_stage), written to out_rgb (host or device per out_location).
+ * Computed by the kernel h2s_process would use for this frame: the tile
+ * kernel's own arithmetic (a debug instance of it) on the tile path, the
+ * generic kernel otherwise (h2s_query_path; H2S_OPT_FAST_PATH = 0 forces the
+ * generic one).  Synchronous. */
 int h2s_debug_float(h2s_ctx *ctx, const h2s_frames *in, int stage,
                     float *out_rgb, int out_location, void *hip_stream);
+
+/* ---- options and introspection ------------------------------------------
+ * h2s_set_option: enum h2s_option.  h2s_query_path: the enum h2s_path that
+ * h2s_process(ctx, in, out, ...) would take with the current params, LUT and
+ * options (negative H2S_E_* on invalid input). */
+int h2s_set_option(h2s_ctx *ctx, int key, int64_t value);
+int h2s_query_path(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out);
 
 /* ---- dynamic peak (params.peak_detect, BT.2390 / spline) -----------------
  * h2s_peak_reset: forget the smoothing state (a new sequence / scene cut).

@@ -44,6 +44,10 @@ class Params(ctypes.Structure):
         ('mastering_max', ctypes.c_double), ('lut_enabled', ctypes.c_int32),
         ('mode', ctypes.c_int32), ('desat_luma', ctypes.c_int32),
         ('peak_detect', ctypes.c_int32),
+        ('chroma_filter', ctypes.c_int32), ('dither', ctypes.c_int32),
+        ('expand', ctypes.c_int32), ('pipeline', ctypes.c_int32),
+        ('knee_offset', ctypes.c_double), ('target_black', ctypes.c_double),
+        ('target_white', ctypes.c_double),
         ('reserved', ctypes.c_int32 * 4),
     ]
 
@@ -72,7 +76,8 @@ def default_params(**kw) -> Params:
     """Reference chain defaults (see include/h2s.h h2s_params_default)."""
     p = Params(transfer_in=0, bits_in=10, bits_out=10, tonemap=6, tm_param=math.nan,
                desat=2.0, peak=0.0, npl=100.0, gamma=1.0, maxcll=0.0, mastering_max=0.0,
-               lut_enabled=1, mode=0, desat_luma=0)
+               lut_enabled=1, mode=0, desat_luma=0, knee_offset=math.nan, target_black=math.nan,
+               target_white=math.nan)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
@@ -110,6 +115,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_peak_stats.restype = ctypes.c_int
         L.oracle_peak_stats.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frames), ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_chroma_taps.restype = None
+        L.oracle_chroma_taps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_preview_tail.restype = ctypes.c_int
         L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
@@ -247,12 +254,27 @@ def resolved(params: Params) -> 'tuple[float, float, np.ndarray]':
     """(peak, param, eq_lut) after vf_tonemap / vf_eq initialisation."""
     peak, param = ctypes.c_double(), ctypes.c_double()
     eq = np.zeros(4096, dtype=np.uint16)
-    rc = lib().oracle_resolved(ctypes.byref(params), ctypes.byref(peak), ctypes.byref(param),
-                               eq.ctypes.data, eq.size)
-    if rc:
-        raise ValueError(f'oracle_resolved failed: {rc}')
-    q = params.bits_out if params.mode == 1 else 8
+    q = lib().oracle_resolved(ctypes.byref(params), ctypes.byref(peak), ctypes.byref(param),
+                              eq.ctypes.data, eq.size)
+    if q < 0:
+        raise ValueError(f'oracle_resolved failed: {q}')
     return peak.value, param.value, eq[:1 << q].copy()
+
+
+def quant_bits(params: Params) -> int:
+    """The depth the chain quantises at: 8 (eq's yuv420p, or the libplacebo
+    branch's nv12) or bits_out (native mode; libplacebo rgba with gamma 1)."""
+    q = lib().oracle_resolved(ctypes.byref(params), None, None, None, 0)
+    if q < 0:
+        raise ValueError(f'oracle_resolved failed: {q}')
+    return q
+
+
+def chroma_taps() -> 'tuple[np.ndarray, np.ndarray]':
+    """The BICUBIC chroma decimation taps (7 horizontal, 8 vertical)."""
+    wx, wy = np.zeros(7, np.float32), np.zeros(8, np.float32)
+    lib().oracle_chroma_taps(wx.ctypes.data, wy.ctypes.data)
+    return wx, wy
 
 
 def tone_curve(params: Params, sig: float) -> float:

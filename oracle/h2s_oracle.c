@@ -23,13 +23,24 @@
  *   S3  zimg rec_1886_inverse_eotf: x < 0 ? 0 : x^(1/2.4) (the pure 2.4
  *       gamma is pinned by tools/generate_lut.py:43-59).
  *   S4  libavfilter/vf_lut3d.c: sanitizef, clip(x*(N-1)), interp_tetrahedral.
- *   S6  swscale gbrpf32 -> yuv420p (auto-inserted before eq): modelled as
- *       BT.709 limited-range matrix, centre-sited 2x2 box chroma,
- *       round-half-up, no dither.  [EXT: model, not pinned]
+ *   S6  swscale gbrpf32 -> yuv420p (auto-inserted before eq): BT.709
+ *       limited-range matrix; chroma filter h2s_params.chroma_filter (BOX:
+ *       centre-sited 2x2 mean, default; BICUBIC: swscale's bicubic B=0 C=0.6
+ *       decimation, left-sited horizontally, centred vertically); rounding
+ *       h2s_params.dither (NONE: half up; ORDERED: ff_dither_8x8_128).
+ *       [EXT: model, not pinned]
  *   S7  libavfilter/vf_eq.c create_lut (gamma only, Y plane only).
- *   S8  swscale planarCopyWrapper 8 -> 10/12 bit: plain shift (tv range).
+ *   S8  swscale 8 -> 10/12 bit: h2s_params.expand (SHIFT, default, or
+ *       REPLICATE: v << s | v >> (8 - s)).  [EXT]
+ * The libplacebo branch (src/utils.py:392-471, h2s_params.pipeline =
+ * LIBPLACEBO) is restated in the same chain: libplacebo's bt2390 (knee
+ * offset, black-point adaptation) or spline against the SDR target
+ * [target_black, target_white], BT.1886 encode with that black level, the
+ * 8-bit rgba download, lut3d's 8-bit path (truncating), and swscale rgba ->
+ * Y'CbCr at the output depth.  PARITY UNPINNED (libplacebo absent).
  * Where a choice cannot be pinned without the bundled ffmpeg it is a named
- * parameter (h2s_params.desat_luma, .mode) — see DESIGN.md "Oracle".
+ * parameter (h2s_params.desat_luma, .mode, .chroma_filter, .dither, .expand,
+ * .knee_offset, .target_black, .target_white) — see DESIGN.md "Oracle".
  */
 #include <float.h>
 #include <math.h>
@@ -67,6 +78,15 @@ typedef struct {
   uint16_t eq_lut[4096];
   const float *lut;
   int lut_n;
+  /* pipeline (resolved: H2S_PIPE_CPU_CHAIN or H2S_PIPE_LIBPLACEBO) */
+  int pipe;
+  int rgba8;            /* libplacebo branch with the LUT: 8-bit rgba + lut3d 8-bit */
+  double tb, tw;        /* SDR target black / white (nits)                  */
+  double knee_off;      /* BT.2390 knee offset                             */
+  double min_lum, bp, bgain; /* BT.2390 black-point adaptation (PQ, source-normalised) */
+  double out_scale;     /* curve output (PQ-normalised linear) -> units of tw */
+  double enc_a, enc_b;  /* libplacebo BT.1886 encode: (x / a)^(1/2.4) - b   */
+  int dither;           /* 1: ordered dither at the swscale 8-bit quantiser */
 } ocfg;
 
 /* ---- S1 helpers -------------------------------------------------------- */
@@ -130,14 +150,19 @@ static float pq_encode_f(float y) {
   return powf((PQ_C1 + PQ_C2 * ym) / (1.0f + PQ_C3 * ym), PQ_M2);
 }
 
-/* BT.2390-8 section 5.4 EETF on the PQ-encoded signal (Lmin = Lb = 0).  The
- * reference reaches BT.2390 only through libplacebo (src/utils.py:62-73,
- * :445-449); that implementation is not restated here: parity unpinned. */
+/* BT.2390 EETF on the PQ-encoded signal as libplacebo's tone_mapping.c
+ * bt2390 computes it (the reference reaches BT.2390 only through libplacebo,
+ * src/utils.py:62-73, :445-449): E1 normalised to the source range, Hermite
+ * knee at ks = (1 + knee_offset) maxLum - knee_offset (libplacebo default
+ * offset 1.0; ITU-R BT.2390's 0.5 is the knee_offset = 0.5 switch), then the
+ * black-point adaptation x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum
+ * for a target black above 0, back to PQ over the source range.  Restated
+ * from the published algorithm; libplacebo is absent: PARITY UNPINNED. */
 static float bt2390_sig(const ocfg *c, float sig) {
   float e1 = pq_encode_f(sig * (float)(c->p->npl / 10000.0));
   float e1n = (e1 - (float)c->src_min) / (float)(c->src_max - c->src_min);
-  /* E1 is clipped to the source range [Lb, Lw] (BT.2390-8 5.4); a NaN from an
-   * overflowed (inf) input counts as above the range */
+  /* E1 is clipped to the source range; a NaN from an overflowed (inf) input
+   * counts as above the range */
   e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);
   float ks = (float)c->ks, ml = (float)c->max_lum;
   float e2 = e1n;
@@ -147,9 +172,14 @@ static float bt2390_sig(const ocfg *c, float sig) {
     e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * ks + (t3 - 2.0f * t2 + t) * (1.0f - ks) +
          (-2.0f * t3 + 3.0f * t2) * ml;
   }
+  if (c->min_lum > 0.0 && e2 < 1.0f) {
+    const float mn = (float)c->min_lum;
+    e2 += mn * powf(1.0f - e2, (float)c->bp);
+    e2 = (float)c->bgain * (e2 - mn) + mn;
+  }
   float e4 = e2 * (float)(c->src_max - c->src_min) + (float)c->src_min;
-  /* back to linear, in units of npl */
-  return st2084_eotf(e4) * (float)(10000.0 / c->p->npl);
+  /* back to linear, in units of the target white */
+  return st2084_eotf(e4) * (float)c->out_scale;
 }
 
 /* libplacebo src/tone_mapping.c "spline" (scaling PL_HDR_PQ), restated from
@@ -180,7 +210,7 @@ static double pq_eotf_dd(double e) {
 static void spline_setup(ocfg *c, double avg_pq) {
   const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
   double smin = pq_encode_d(0.0), smax = pq_encode_d(c->peak * 100.0 / 10000.0);
-  double dmin = pq_encode_d(0.0), dmax = pq_encode_d(c->p->npl / 10000.0);
+  double dmin = pq_encode_d(c->tb / 10000.0), dmax = pq_encode_d(c->tw / 10000.0);
   double sk = avg_pq > 0.0 ? avg_pq : smin + (smax - smin) * kdef;
   double lo = smin + (smax - smin) * kmin, hi = smin + (smax - smin) * kmax;
   sk = sk < lo ? lo : (sk > hi ? hi : sk);
@@ -215,7 +245,7 @@ static float spline_pq_f(const ocfg *c, float e) {
 
 static float spline_sig(const ocfg *c, float sig) {
   float e2 = spline_pq_f(c, pq_encode_f(sig * (float)(c->p->npl / 10000.0)));
-  return st2084_eotf(e2) * (float)(10000.0 / c->p->npl);
+  return st2084_eotf(e2) * (float)c->out_scale;
 }
 
 #define MIX(x, y, a) (x) * (1 - (a)) + (y) * (a)
@@ -313,11 +343,8 @@ static rgbf lat(const ocfg *c, int ri, int gi, int bi) {
   return v;
 }
 
-static rgbf lut3d_tetra(const ocfg *c, rgbf in) {
-  const float lut_max = (float)(c->lut_n - 1);
-  const float sr = 1.0f * lut_max, sg = 1.0f * lut_max, sb = 1.0f * lut_max;
-  rgbf s = {clipf(sanitizef(in.r) * sr, 0, lut_max), clipf(sanitizef(in.g) * sg, 0, lut_max),
-            clipf(sanitizef(in.b) * sb, 0, lut_max)};
+/* tetrahedral blend at lattice coordinates s (already clipped to [0, N-1]) */
+static rgbf lut3d_tetra_at(const ocfg *c, rgbf s) {
   int n = c->lut_n;
   int pr = (int)s.r, pg = (int)s.g, pb = (int)s.b;
   int nr = pr + 1 < n - 1 ? pr + 1 : n - 1;
@@ -358,6 +385,14 @@ static rgbf lut3d_tetra(const ocfg *c, rgbf in) {
   return o;
 }
 
+static rgbf lut3d_tetra(const ocfg *c, rgbf in) {
+  const float lut_max = (float)(c->lut_n - 1);
+  const float sr = 1.0f * lut_max, sg = 1.0f * lut_max, sb = 1.0f * lut_max;
+  rgbf s = {clipf(sanitizef(in.r) * sr, 0, lut_max), clipf(sanitizef(in.g) * sg, 0, lut_max),
+            clipf(sanitizef(in.b) * sb, 0, lut_max)};
+  return lut3d_tetra_at(c, s);
+}
+
 /* lut_enabled = 0: the legacy closed-form gamut step
  * (FFMPEG_FILTER_LEGACY_NO_LUT, src/utils.py:57-60: zscale ...:p=bt709),
  * i.e. linear BT.2020 -> BT.709 matrix (tools/generate_lut.py:36-40), then
@@ -366,7 +401,40 @@ static const float M2020_709[3][3] = {{1.6604910021f, -0.5876411388f, -0.0728498
                                       {-0.1245504745f, 1.1328998971f, -0.0083494226f},
                                       {-0.0181507634f, -0.1005788980f, 1.1187296614f}};
 
-/* ---- one pixel through S1(after upsample)..S4 --------------------------- */
+/* libplacebo branch: BT.1886 encode against the target's black level
+ * (libplacebo's PL_COLOR_TRC_BT_1886 delinearisation: lb = (black/white)^(1/2.4),
+ * a = (1 - lb)^2.4, b = lb / (1 - lb); pure 2.4 gamma when black = 0). */
+static float lp_encode(const ocfg *c, float x) {
+  if (!(x > 0.0f)) x = 0.0f;
+  return powf(x / (float)c->enc_a, 1.0f / 2.4f) - (float)c->enc_b;
+}
+
+/* libplacebo branch: the 8-bit rgba download (round to nearest, no dither:
+ * libplacebo's default blue-noise dither is not restated) */
+static int rgba8_q(float v) {
+  v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  return (int)floorf(v * 255.0f + 0.5f);
+}
+
+/* vf_lut3d's 8-bit packed path (interp_8_tetrahedral): coordinate
+ * clip((q * (1/255)) * (N-1), 0, N-1), tetrahedral blend, output truncated
+ * to 8 bits (av_clip_uint8 of the float product's integer conversion) */
+static rgbf lut3d_8bit(const ocfg *c, int r8, int g8, int b8) {
+  const float scale_f = 1.0f / 255.0f, lut_max = (float)(c->lut_n - 1);
+  rgbf s = {clipf((float)r8 * scale_f * lut_max, 0, lut_max), clipf((float)g8 * scale_f * lut_max, 0, lut_max),
+            clipf((float)b8 * scale_f * lut_max, 0, lut_max)};
+  rgbf o = lut3d_tetra_at(c, s);
+  int R = (int)(o.r * 255.0f), G = (int)(o.g * 255.0f), B = (int)(o.b * 255.0f);
+  rgbf q = {(float)(R < 0 ? 0 : (R > 255 ? 255 : R)), (float)(G < 0 ? 0 : (G > 255 ? 255 : G)),
+            (float)(B < 0 ? 0 : (B > 255 ? 255 : B))};
+  return q;
+}
+
+/* ---- one pixel through S1(after upsample)..S4 ---------------------------
+ * CPU chain: stage 3 = BT.1886-inverse R'G'B', stage 4 = lut3d output.
+ * libplacebo branch: stage 3 = BT.1886 (target black) R'G'B' before the
+ * download, stage 4 = lut3d's 8-bit output / 255 (LUT on) or the encoded
+ * BT.709 R'G'B' (LUT off: libplacebo's own gamut conversion, clipped). */
 static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf *dbg) {
   (void)dbg;
   rgbf e;
@@ -392,6 +460,25 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf 
   rgbf t = tonemap_px(c, l);
   if (upto == H2S_STAGE_TONEMAP) return t;
   rgbf g;
+  if (c->pipe == H2S_PIPE_LIBPLACEBO) {
+    if (c->p->lut_enabled) {
+      g.r = lp_encode(c, t.r);
+      g.g = lp_encode(c, t.g);
+      g.b = lp_encode(c, t.b);
+      if (upto == H2S_STAGE_GAMMA) return g;
+      rgbf q = lut3d_8bit(c, rgba8_q(g.r), rgba8_q(g.g), rgba8_q(g.b));
+      rgbf o = {q.r / 255.0f, q.g / 255.0f, q.b / 255.0f};
+      return o;
+    }
+    rgbf m;
+    m.r = M2020_709[0][0] * t.r + M2020_709[0][1] * t.g + M2020_709[0][2] * t.b;
+    m.g = M2020_709[1][0] * t.r + M2020_709[1][1] * t.g + M2020_709[1][2] * t.b;
+    m.b = M2020_709[2][0] * t.r + M2020_709[2][1] * t.g + M2020_709[2][2] * t.b;
+    g.r = clipf(lp_encode(c, m.r), 0.0f, 1.0f);
+    g.g = clipf(lp_encode(c, m.g), 0.0f, 1.0f);
+    g.b = clipf(lp_encode(c, m.b), 0.0f, 1.0f);
+    return g;
+  }
   if (c->p->lut_enabled) {
     g.r = bt1886_inverse(t.r);
     g.g = bt1886_inverse(t.g);
@@ -417,7 +504,23 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   c->lut_n = n;
   if (p->bits_in != 10 && p->bits_in != 12) return H2S_E_UNSUPPORTED;
   if (p->bits_out != 8 && p->bits_out != 10 && p->bits_out != 12) return H2S_E_UNSUPPORTED;
-  c->q_bits = p->mode == H2S_MODE_NATIVE ? p->bits_out : 8;
+  /* the two chains of the reference (include/h2s.h enum h2s_pipeline) */
+  c->pipe = p->pipeline;
+  if (c->pipe == H2S_PIPE_AUTO)
+    c->pipe = (p->tonemap == H2S_TM_BT2390 || p->tonemap == H2S_TM_SPLINE) ? H2S_PIPE_LIBPLACEBO : H2S_PIPE_CPU_CHAIN;
+  if (c->pipe == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
+    return H2S_E_UNSUPPORTED; /* libplacebo's own hable/mobius/reinhard curves are not restated */
+  c->rgba8 = c->pipe == H2S_PIPE_LIBPLACEBO && p->lut_enabled;
+  /* quantisation depth: the CPU chain's eq forces yuv420p (compat8); the
+   * libplacebo branch with the LUT and gamma 1 has no eq, so its rgba frame
+   * goes straight to the output -pix_fmt; its LUT-off form downloads nv12 */
+  if (p->mode == H2S_MODE_NATIVE)
+    c->q_bits = p->bits_out;
+  else if (c->rgba8 && p->gamma == 1.0)
+    c->q_bits = p->bits_out;
+  else
+    c->q_bits = 8;
+  c->dither = p->dither == H2S_DITHER_ORDERED && c->q_bits == 8;
 
   /* vf_tonemap init: parameter defaults */
   double param = p->tm_param;
@@ -471,11 +574,28 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   c->m_bcb = (float)(2.0 * (1.0 - kb));
   c->lin_scale = (float)((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl);
 
-  /* BT.2390 constants: source [0, peak*100 nits], target [0, npl nits] */
+  /* SDR target: the CPU chain's tone curve output is relative to npl with
+   * no black level; libplacebo targets its SDR white (203 nits) with a
+   * 1000:1 contrast black (PL_COLOR_SDR_WHITE / PL_COLOR_SDR_CONTRAST) */
+  int lp = c->pipe == H2S_PIPE_LIBPLACEBO;
+  c->tw = isnan(p->target_white) || !(p->target_white > 0) ? (lp ? 203.0 : p->npl) : p->target_white;
+  c->tb = isnan(p->target_black) ? (lp ? c->tw / 1000.0 : 0.0) : p->target_black;
+  c->knee_off = isnan(p->knee_offset) ? 1.0 : p->knee_offset;
+  c->out_scale = 10000.0 / c->tw;
+  {
+    double lb = pow(c->tb / c->tw, 1.0 / 2.4);
+    c->enc_a = pow(1.0 - lb, 2.4);
+    c->enc_b = lb / (1.0 - lb);
+  }
+  /* BT.2390 constants (libplacebo bt2390): source [0, peak*100 nits] and
+   * target [black, white] in PQ, normalised to the source range */
   c->src_min = pq_encode_d(0.0);
   c->src_max = pq_encode_d(peak * 100.0 / 10000.0);
-  c->max_lum = (pq_encode_d(p->npl / 10000.0) - c->src_min) / (c->src_max - c->src_min);
-  c->ks = 1.5 * c->max_lum - 0.5;
+  c->max_lum = (pq_encode_d(c->tw / 10000.0) - c->src_min) / (c->src_max - c->src_min);
+  c->min_lum = c->tb > 0.0 ? (pq_encode_d(c->tb / 10000.0) - c->src_min) / (c->src_max - c->src_min) : 0.0;
+  c->ks = (1.0 + c->knee_off) * c->max_lum - c->knee_off;
+  c->bp = c->min_lum > 0.0 ? fmin(1.0 / c->min_lum, 4.0) : 4.0;
+  c->bgain = c->max_lum < 1.0 ? 1.0 / (1.0 + c->min_lum / c->max_lum * pow(1.0 - c->max_lum, c->bp)) : 1.0;
   /* spline: contrast = tm_param (NaN -> libplacebo's default 0.5) */
   c->sp_contrast = isnan(p->tm_param) ? 0.5 : p->tm_param;
   spline_setup(c, 0.0);
@@ -552,39 +672,158 @@ static inline float upsample(const ocfg *c, const h2s_frames *in, int plane, int
 /* ---- S6 model + S7 + S8 -------------------------------------------------- */
 static const float K709_R = 0.2126f, K709_G = 0.7152f, K709_B = 0.0722f;
 
-static inline int quant(float v, int qmax) {
-  int i = (int)floorf(v + 0.5f);
+/* swscale's 8x8 ordered dither (libswscale ff_dither_8x8_128, in 1/128 of
+ * an output LSB): the H2S_DITHER_ORDERED switch of the 8-bit quantiser */
+static const uint8_t DITHER8[8][8] = {
+    {36, 68, 60, 92, 34, 66, 58, 90},   {100, 4, 124, 28, 98, 2, 122, 26},
+    {52, 84, 44, 76, 50, 82, 42, 74},   {116, 20, 108, 12, 114, 18, 106, 10},
+    {32, 64, 56, 88, 38, 70, 62, 94},   {96, 0, 120, 24, 102, 6, 126, 30},
+    {48, 80, 40, 72, 54, 86, 46, 78},   {112, 16, 104, 8, 118, 22, 110, 14}};
+
+/* the quantiser's rounding offset at sample (x, y) of its plane */
+static inline float qoff(const ocfg *c, int x, int y) {
+  return c->dither ? (float)DITHER8[y & 7][x & 7] * (1.0f / 128.0f) : 0.5f;
+}
+
+static inline int quant_o(float v, float off, int qmax) {
+  int i = (int)floorf(v + off);
   return i < 0 ? 0 : (i > qmax ? qmax : i);
 }
 
-static void process_quad_row(const ocfg *c, const h2s_frames *in, const h2s_frames *out, int f, int cy) {
-  const h2s_params *p = c->p;
-  int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
-  int q = c->q_bits, qmax = (1 << q) - 1;
-  float s = (float)(1 << (q - 8));
-  int shift_out = p->mode == H2S_MODE_NATIVE ? 0 : p->bits_out - 8;
+/* S8: an 8-bit code (after eq) to the output depth */
+static inline int expand8(const ocfg *c, int v, int shift) {
+  if (!shift) return v;
+  if (c->p->expand == H2S_EXPAND_REPLICATE) return (v << shift) | (v >> (8 - shift));
+  return v << shift;
+}
+
+/* one pixel -> S6 quantiser inputs: Y code (16 + 219 Y) s and the pixel's
+ * chroma as normalised Cb / Cr (the 4:2:0 sample is 128 s + 224 s * filter) */
+typedef struct {
+  float y, cb, cr;
+} yuvf;
+
+static yuvf px_yuv(const ocfg *c, const h2s_frames *in, int f, int x, int y) {
+  int cw = in->width / 2, ch = in->height / 2;
+  float s = (float)(1 << (c->q_bits - 8));
   const float cbr = (float)(-0.2126 / 1.8556), cbg = (float)(-0.7152 / 1.8556), cbb = (float)(0.9278 / 1.8556);
   const float crr = (float)(0.7874 / 1.5748), crg = (float)(-0.7152 / 1.5748), crb = (float)(-0.0722 / 1.5748);
+  float yv = (float)rd(in, 0, f, x, y) * c->y_scale + c->y_off;
+  float cb = upsample(c, in, 1, f, x, y, cw, ch);
+  float cr = upsample(c, in, 2, f, x, y, cw, ch);
+  rgbf o = chain_px(c, yv, cb, cr, 99, NULL);
+  float R = clipf(o.r, 0.0f, 1.0f), G = clipf(o.g, 0.0f, 1.0f), B = clipf(o.b, 0.0f, 1.0f);
+  float Y = K709_R * R + K709_G * G + K709_B * B;
+  yuvf r = {(16.0f + 219.0f * Y) * s, cbr * R + cbg * G + cbb * B, crr * R + crg * G + crb * B};
+  return r;
+}
+
+static void store_luma(const ocfg *c, const h2s_frames *out, int f, int x, int y, float yc) {
+  int qmax = (1 << c->q_bits) - 1, shift = c->p->bits_out - c->q_bits;
+  int yq = quant_o(yc, qoff(c, x, y), qmax);
+  wr(out, 0, f, x, y, expand8(c, (int)c->eq_lut[yq], shift));
+}
+
+static void store_chroma(const ocfg *c, const h2s_frames *out, int f, int cx, int cy, float cb, float cr) {
+  int qmax = (1 << c->q_bits) - 1, shift = c->p->bits_out - c->q_bits;
+  float s = (float)(1 << (c->q_bits - 8)), o = qoff(c, cx, cy);
+  wr(out, 1, f, cx, cy, expand8(c, quant_o((128.0f + 224.0f * cb) * s, o, qmax), shift));
+  wr(out, 2, f, cx, cy, expand8(c, quant_o((128.0f + 224.0f * cr) * s, o, qmax), shift));
+}
+
+/* BOX chroma: one chroma row of quads; the 2x2 mean in (c00 + c01) + (c10 + c11) order */
+static void process_quad_row(const ocfg *c, const h2s_frames *in, const h2s_frames *out, int f, int cy) {
+  int cw = in->width / 2;
   for (int cx = 0; cx < cw; cx++) {
     float cbs[4], crs[4];
     for (int k = 0; k < 4; k++) {
       int x = 2 * cx + (k & 1), y = 2 * cy + (k >> 1);
-      float yv = (float)rd(in, 0, f, x, y) * c->y_scale + c->y_off;
-      float cb = upsample(c, in, 1, f, x, y, cw, ch);
-      float cr = upsample(c, in, 2, f, x, y, cw, ch);
-      rgbf o = chain_px(c, yv, cb, cr, 99, NULL);
-      float R = clipf(o.r, 0.0f, 1.0f), G = clipf(o.g, 0.0f, 1.0f), B = clipf(o.b, 0.0f, 1.0f);
-      float Y = K709_R * R + K709_G * G + K709_B * B;
-      cbs[k] = cbr * R + cbg * G + cbb * B;
-      crs[k] = crr * R + crg * G + crb * B;
-      int yq = quant((16.0f + 219.0f * Y) * s, qmax);
-      wr(out, 0, f, x, y, (int)c->eq_lut[yq] << shift_out);
+      yuvf v = px_yuv(c, in, f, x, y);
+      cbs[k] = v.cb, crs[k] = v.cr;
+      store_luma(c, out, f, x, y, v.y);
     }
     float cb = ((cbs[0] + cbs[1]) + (cbs[2] + cbs[3])) * 0.25f;
     float cr = ((crs[0] + crs[1]) + (crs[2] + crs[3])) * 0.25f;
-    wr(out, 1, f, cx, cy, quant((128.0f + 224.0f * cb) * s, qmax) << shift_out);
-    wr(out, 2, f, cx, cy, quant((128.0f + 224.0f * cr) * s, qmax) << shift_out);
+    store_chroma(c, out, f, cx, cy, cb, cr);
   }
+}
+
+/* swscale SWS_BICUBIC kernel, B = 0, C = 0.6 (also the preview resize) */
+static double o_bicubic(double x) {
+  const double B = 0.0, C = 0.6;
+  x = fabs(x);
+  if (x < 1.0) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) / 6.0;
+  if (x < 2.0) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) / 6.0;
+  return 0.0;
+}
+
+/* BICUBIC chroma decimation taps, normalised, as float: horizontal 7 taps at
+ * luma offsets -3..3 around the left-sited position 2cx; vertical 8 taps at
+ * offsets -3..4 around the centre-sited position 2cy + 0.5 */
+void oracle_chroma_taps(float *wx7, float *wy8) {
+  double sx = 0, sy = 0, tx[7], ty[8];
+  for (int i = 0; i < 7; i++) sx += (tx[i] = o_bicubic((i - 3) / 2.0));
+  for (int j = 0; j < 8; j++) sy += (ty[j] = o_bicubic((j - 3 - 0.5) / 2.0));
+  for (int i = 0; i < 7; i++) wx7[i] = (float)(tx[i] / sx);
+  for (int j = 0; j < 8; j++) wy8[j] = (float)(ty[j] / sy);
+}
+
+/* BICUBIC: per frame, every pixel's chroma into a 4:4:4 scratch (luma stored
+ * on the way), then the separable decimation, horizontal pass first, taps
+ * edge-clamped, summed in tap order */
+static int process_frame_bicubic(const ocfg *c, const h2s_frames *in, const h2s_frames *out, int f, int nthreads) {
+  int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
+  float *cb = (float *)malloc(sizeof(float) * 2 * (size_t)W * H);
+  float *hb = (float *)malloc(sizeof(float) * 2 * (size_t)cw * H);
+  if (!cb || !hb) {
+    free(cb);
+    free(hb);
+    return H2S_E_OOM;
+  }
+  float *cr = cb + (size_t)W * H, *hr = hb + (size_t)cw * H;
+  float wx[7], wy[8];
+  oracle_chroma_taps(wx, wy);
+  (void)nthreads;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      yuvf v = px_yuv(c, in, f, x, y);
+      cb[(size_t)y * W + x] = v.cb, cr[(size_t)y * W + x] = v.cr;
+      store_luma(c, out, f, x, y, v.y);
+    }
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int y = 0; y < H; y++)
+    for (int k = 0; k < cw; k++) {
+      float su = 0.0f, sv = 0.0f;
+      for (int i = 0; i < 7; i++) {
+        int x = 2 * k - 3 + i;
+        x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
+        su += wx[i] * cb[(size_t)y * W + x];
+        sv += wx[i] * cr[(size_t)y * W + x];
+      }
+      hb[(size_t)y * cw + k] = su, hr[(size_t)y * cw + k] = sv;
+    }
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int m = 0; m < ch; m++)
+    for (int k = 0; k < cw; k++) {
+      float su = 0.0f, sv = 0.0f;
+      for (int j = 0; j < 8; j++) {
+        int y = 2 * m - 3 + j;
+        y = y < 0 ? 0 : (y > H - 1 ? H - 1 : y);
+        su += wy[j] * hb[(size_t)y * cw + k];
+        sv += wy[j] * hr[(size_t)y * cw + k];
+      }
+      store_chroma(c, out, f, k, m, su, sv);
+    }
+  free(cb);
+  free(hb);
+  return 0;
 }
 
 /* ---- exported entry points (ctypes) ------------------------------------- */
@@ -600,9 +839,16 @@ int oracle_process_knee(const h2s_params *p, const float *lut, int lut_n, const 
       in->bits != p->bits_in || out->bits != p->bits_out)
     return H2S_E_INVALID_ARG;
   int ch = in->height / 2;
-  int64_t rows = (int64_t)nframes * ch;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  if (p->chroma_filter == H2S_CHROMA_BICUBIC) {
+    for (int f = 0; f < nframes; f++)
+      if ((rc = process_frame_bicubic(&c, in, out, f, nthreads))) return rc;
+    return 0;
+  }
+  int64_t rows = (int64_t)nframes * ch;
+#ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 4)
 #endif
   for (int64_t r = 0; r < rows; r++) process_quad_row(&c, in, out, (int)(r / ch), (int)(r % ch));
@@ -623,13 +869,21 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
   if (rc) return rc;
   int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
   size_t plane = (size_t)W * H;
+  const float s = (float)(1 << (c.q_bits - 8));
   for (int y = 0; y < H; y++)
     for (int x = 0; x < W; x++) {
+      size_t i = (size_t)y * W + x;
+      if (stage == H2S_STAGE_YUV) {
+        yuvf v = px_yuv(&c, in, 0, x, y);
+        out_rgb[i] = v.y;
+        out_rgb[plane + i] = 224.0f * s * v.cb;
+        out_rgb[2 * plane + i] = 224.0f * s * v.cr;
+        continue;
+      }
       float yv = (float)rd(in, 0, 0, x, y) * c.y_scale + c.y_off;
       float cb = upsample(&c, in, 1, 0, x, y, cw, ch);
       float cr = upsample(&c, in, 2, 0, x, y, cw, ch);
       rgbf o = chain_px(&c, yv, cb, cr, stage, NULL);
-      size_t i = (size_t)y * W + x;
       out_rgb[i] = o.r;
       out_rgb[plane + i] = o.g;
       out_rgb[2 * plane + i] = o.b;
@@ -637,7 +891,8 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
   return 0;
 }
 
-/* resolved constants, for tests of the parameter logic */
+/* resolved constants, for tests of the parameter logic; returns the
+ * quantisation depth q (8 or bits_out) or a negative H2S_E_* code */
 int oracle_resolved(const h2s_params *p, double *peak, double *param, uint16_t *eq_lut, int eq_cap) {
   ocfg c;
   int rc = resolve(&c, p, NULL, 0);
@@ -646,7 +901,7 @@ int oracle_resolved(const h2s_params *p, double *peak, double *param, uint16_t *
   if (param) *param = c.param;
   int qn = 1 << c.q_bits;
   for (int i = 0; i < qn && i < eq_cap; i++) eq_lut[i] = c.eq_lut[i];
-  return 0;
+  return c.q_bits;
 }
 
 /* single-pixel tone-curve probe: sig -> sig' (for known-answer tests) */
@@ -671,14 +926,6 @@ float oracle_hlg_inverse_oetf(float x) { return arib_b67_inverse_oetf(x); }
  * GPU preview follows: swscale SWS_BICUBIC (B=0, C=0.6), centre-aligned,
  * support widened by the ratio when downscaling, edge-clamped; BT.709
  * limited -> full-range RGB with nearest chroma; PIL's round-half-even LUT. */
-static double o_bicubic(double x) {
-  const double B = 0.0, C = 0.6;
-  x = fabs(x);
-  if (x < 1.0) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) / 6.0;
-  if (x < 2.0) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) / 6.0;
-  return 0.0;
-}
-
 static void o_resize(const uint8_t *src, int sw, int sh, uint8_t *dst, int ow, int oh) {
   const double scx = (double)sw / ow, scy = (double)sh / oh;
   const double fx = scx > 1 ? scx : 1, fy = scy > 1 ? scy : 1;

@@ -39,11 +39,15 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_defaults():
     L = _abi.lib()
-    assert L.h2s_abi_version() == 1
+    assert L.h2s_abi_version() == _abi.ABI_VERSION == 2
     p = _abi.default_params()
     assert (p.transfer_in, p.bits_in, p.bits_out, p.tonemap, p.desat, p.npl, p.gamma, p.lut_enabled) == \
         (0, 10, 10, 6, 2.0, 100.0, 1.0, 1)
     assert p.tm_param != p.tm_param  # NaN = filter default
+    # [EXT] switches default to the round-1 models; libplacebo targets NaN = branch default
+    assert (p.chroma_filter, p.dither, p.expand, p.pipeline) == (0, 0, 0, 0)
+    for v in (p.knee_offset, p.target_black, p.target_white):
+        assert v != v
 
 
 PROBE = r'''
@@ -51,9 +55,10 @@ PROBE = r'''
 #include <stdio.h>
 #include "h2s.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(h2s_params), offsetof(h2s_params, tm_param),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(h2s_params), offsetof(h2s_params, tm_param),
          offsetof(h2s_params, lut_enabled), offsetof(h2s_params, desat_luma), sizeof(h2s_frames),
-         offsetof(h2s_frames, width));
+         offsetof(h2s_frames, width), offsetof(h2s_params, pipeline), offsetof(h2s_params, knee_offset),
+         offsetof(h2s_params, target_white));
   return 0;
 }
 '''
@@ -67,7 +72,8 @@ def test_struct_layout_matches_c(tmp_path):
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     for P, F in ((_abi.H2SParams, _abi.H2SFrames), (oracle.Params, oracle.Frames)):
         want = [ctypes.sizeof(P), P.tm_param.offset, P.lut_enabled.offset, P.desat_luma.offset,
-                ctypes.sizeof(F), F.width.offset]
+                ctypes.sizeof(F), F.width.offset, P.pipeline.offset, P.knee_offset.offset,
+                P.target_white.offset]
         assert got == want
 
 
@@ -87,6 +93,8 @@ def test_null_handling_without_device():
     assert L.h2s_process(None, None, None, 1, None) == _abi.H2S_E_INVALID_ARG
     L.h2s_destroy(None)
     assert L.h2s_cube_format(1, None, 0) == _abi.H2S_E_INVALID_ARG
+    assert L.h2s_set_option(None, _abi.OPT_FAST_PATH, 0) == _abi.H2S_E_INVALID_ARG
+    assert L.h2s_query_path(None, None, None) == _abi.H2S_E_INVALID_ARG
     with pytest.raises(ValueError):
         _abi.raise_for(_abi.H2S_E_UNSUPPORTED, 'x')
     with pytest.raises(FileNotFoundError):

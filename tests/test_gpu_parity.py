@@ -57,17 +57,32 @@ def run_both(tm, params, kind, W, H, nframes=2, lut_n=65, seed=11):
 def assert_close_int(params, got, want, W, H, max_frac=5e-3):
     """Chroma: |diff| <= one quantisation step.  Luma: eq runs after the
     quantiser, so the bound is +-1 step *before* eq: got must lie between
-    eq[q-1] and eq[q+1] where eq[q] == want (eq is monotonic)."""
-    q = params.bits_out if params.mode == 'native' else 8
+    eq[q-1] and eq[q+1] where eq[q] == want (eq is monotonic).
+
+    The libplacebo branch quantises twice before the output (the 8-bit rgba
+    download and lut3d's truncating 8-bit output): a float-rounding flip there
+    moves one R'G'B' channel by 1/255, i.e. Y'CbCr at depth q by at most
+    ceil(224 * 2^(q-8) / 255) + 1 steps — that is its bound."""
+    op = oracle.params_from(params.to_c())
+    q = oracle.quant_bits(op)
+    if params.resolved_pipeline() == 'libplacebo' and params.lut_enabled:
+        step = 1 << (params.bits_out - q)
+        bound = (-(-224 * (1 << (q - 8)) // 255) + 1) * step
+        d = np.abs(got - want)
+        assert d.max(initial=0) <= bound, f'max diff {d.max()} > {bound} (one 8-bit R\'G\'B\' step)'
+        frac = float((d > step).mean())
+        assert frac <= max_frac, f'{frac:.3%} of samples beyond one step'
+        return
     shift = params.bits_out - q if params.bits_out >= q else 0
     step = 1 << shift
     ysz = W * H
     gy, wy = got[:, :ysz] >> shift, want[:, :ysz] >> shift
     gc, wc = got[:, ysz:], want[:, ysz:]
-    assert np.all(got % step == 0) and np.all(want % step == 0)
+    if params.expand == 'shift':
+        assert np.all(got % step == 0) and np.all(want % step == 0)
     dc = np.abs(gc - wc)
     assert dc.max(initial=0) <= step, f'chroma max diff {dc.max()} > step {step}'
-    eq = oracle.resolved(oracle.params_from(params.to_c()))[2].astype(np.int64)
+    eq = oracle.resolved(op)[2].astype(np.int64)
     lo_i = np.searchsorted(eq, wy, side='left')            # first q with eq[q] == want
     hi_i = np.searchsorted(eq, wy, side='right') - 1       # last q with eq[q] == want
     assert np.all(eq[np.clip(lo_i, 0, len(eq) - 1)] == wy), 'oracle luma not in eq table'
@@ -158,25 +173,67 @@ def test_lut_disabled_closed_form(tm):
     assert_close_int(params, got, want, *src_wh)
 
 
-@pytest.mark.parametrize('lut_n', [2, 17, 33, 65])
+@pytest.mark.parametrize('lut_n', [2, 17, 33, 65, 129, 177, 178, 200, 256])
 def test_lut_sizes(tm, lut_n):
+    """Every lut3d size (MAX_LEVEL 256).  The tile kernel forms lattice byte
+    offsets in float32 (exact below 2^26 for multiples of 4, i.e. N <= 177);
+    larger lattices take the generic kernel (h2s_query_path)."""
+    from hdr2sdr import _abi
     params = hdr2sdr.TonemapParams(tonemapper='mobius')
     got, want, src_wh = run_both(tm, params, 'uniform', 64, 32, lut_n=lut_n)
     assert_close_int(params, got, want, *src_wh)
+    src = hdr2sdr.FrameBatch.empty_torch(1, 64, 32, 10, 'cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(1, 64, 32, 10, 'cuda')
+    assert tm.query_path(src, dst) == (_abi.PATH_TILE if lut_n <= 177 else _abi.PATH_GENERIC)
 
 
-@pytest.mark.parametrize('stage', [1, 2, 3, 4])
-@pytest.mark.parametrize('transfer,bits', [('smpte2084', 10), ('arib-std-b67', 12)])
-def test_float_intermediates_within_1e3(tm, stage, transfer, bits):
-    params = hdr2sdr.TonemapParams(tonemapper='hable', bits_in=bits, bits_out=bits, transfer=transfer)
-    src = synth_frames('uniform', 1, 64, 32, bits, device='cpu', seed=3)
+# 1e-3 relative on the float path (north_star), per stage, on the kernel that
+# produces the output: k_tile's own debug instance (H2S_OPT_FAST_PATH 1, the
+# tile path) and the generic kernel (FAST_PATH 0).  Absolute floors, all set
+# by the first PQ table segment (E < 1/128, below 0.0015 nits), where the
+# cubic's absolute error is 7.3e-8 in units of npl (profiles: DESIGN.md §2):
+#   stages 1/2 (linear, units of npl): 2e-7;
+#   stage 3/4 (gamma-encoded / post-LUT R'G'B'): 3.2e-4 at most in gamma space
+#     through x^(1/2.4) near black, and the LUT's slopes up to ~1.7: 6e-4;
+#   stage 5 (quantiser inputs, code units at depth q): 219 * 2^(q-8) * 3e-4.
+FLOAT_CFGS = {
+    'C2_hable_pq10': dict(tonemapper='hable', gamma=2.2, bits_out=10),
+    'C3_bt2390_pq10_cpu': dict(tonemapper='bt.2390', pipeline='cpu', bits_out=10),
+    'C5_hable_hlg12': dict(tonemapper='hable', bits_in=12, bits_out=12, transfer='arib-std-b67'),
+    'C4_mobius_native': dict(tonemapper='mobius', bits_out=10, mode='native'),
+}
+
+
+@pytest.mark.parametrize('stage', [1, 2, 3, 4, 5])
+@pytest.mark.parametrize('kind', ['uniform', 'edges', 'ramp'])
+@pytest.mark.parametrize('cfg', sorted(FLOAT_CFGS))
+@pytest.mark.parametrize('kernel', ['k_tile', 'k_debug'])
+def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
+    from hdr2sdr import _abi
+    params = hdr2sdr.TonemapParams(**FLOAT_CFGS[cfg])
+    W, H = 128, 64
+    src = synth_frames(kind, 1, W, H, params.bits_in, device='cpu', seed=3)
     tm.set_params(params)
     tm.set_lut(lattice(65))
-    got = tm.debug_float(src.to_torch('cuda'), stage)
-    want = oracle.debug_float(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, 64, 32, stage)
+    tm.set_option(_abi.OPT_FAST_PATH, 1 if kernel == 'k_tile' else 0)
+    try:
+        dsrc = src.to_torch('cuda')
+        path = tm.query_path(dsrc, hdr2sdr.FrameBatch.empty_torch(1, W, H, params.bits_out, 'cuda'))
+        assert path == (_abi.PATH_TILE if kernel == 'k_tile' else _abi.PATH_GENERIC)
+        got = tm.debug_float(dsrc, stage)
+    finally:
+        tm.set_option(_abi.OPT_FAST_PATH, 1)
+    op = oracle.params_from(params.to_c())
+    want = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, stage).astype(np.float64)
+    if stage == 3 and kernel == 'k_tile':
+        want = np.clip(want, 0.0, 1.0)      # k_tile clamps x to [0, 1) before the power (lattice coordinate)
+    q = oracle.quant_bits(op)
+    floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
     err = np.abs(got.astype(np.float64) - want)
-    tol = 1e-3 * np.abs(want) + 1e-5
-    assert np.all(err <= tol), f'stage {stage}: worst rel err {float((err / (np.abs(want) + 1e-12)).max()):.3g}'
+    tol = 1e-3 * np.abs(want) + floor
+    bad = err > tol
+    assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {floor:g}; '
+                           f'worst err {float(err.max()):.3g} at want {float(want.flat[int(err.argmax())]):.4g}')
 
 
 def test_host_memory_path_equals_device_path(tm):

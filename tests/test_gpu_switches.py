@@ -1,0 +1,181 @@
+"""GPU parity for the switchable [EXT] stages and the reference's libplacebo
+branch (src/utils.py:392-471).
+
+None of these can be pinned without the bundled ffmpeg / libplacebo: each
+switch is a named model in the oracle (oracle/h2s_oracle.c) and in libh2s, so
+a box with the real binaries can settle it without a kernel rewrite.  Here the
+HIP path must match the oracle's restatement of every switch value, and the
+switches must actually change the output."""
+import numpy as np
+import pytest
+
+import oracle
+import hdr2sdr
+from hdr2sdr import _abi
+from hdr2sdr.synth import synth_frames
+
+from test_gpu_parity import assert_close_int, lattice, run_both
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def tm():
+    t = hdr2sdr.Tonemapper(0)
+    yield t
+    t.close()
+
+
+def _path(tm, params, W, H):
+    src = hdr2sdr.FrameBatch.empty_torch(1, W, H, params.bits_in, 'cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(1, W, H, params.bits_out, 'cuda')
+    return tm.query_path(src, dst)
+
+
+# ---- S6 chroma filter (App. B.4) -------------------------------------------
+@pytest.mark.parametrize('kind', ['smooth', 'uniform', 'edges'])
+@pytest.mark.parametrize('W,H,bits_out', [(128, 64, 10), (70, 18, 8), (2, 2, 10), (6, 10, 12)])
+def test_bicubic_chroma_matches_oracle(tm, W, H, bits_out, kind):
+    """Two-pass path: per-pixel chroma to a 4:4:4 scratch, then the 7 x 8-tap
+    left/centre-sited bicubic decimation, edge-clamped (tiny frames: every
+    tap clamps)."""
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out, chroma_filter='bicubic')
+    got, want, wh = run_both(tm, params, kind, W, H, nframes=2)
+    assert_close_int(params, got, want, *wh)
+    assert _path(tm, params, W, H) == _abi.PATH_TWO_PASS
+
+
+def test_bicubic_taps_are_the_swscale_kernel():
+    wx, wy = oracle.chroma_taps()
+    assert wx.sum() == pytest.approx(1.0, abs=1e-6) and wy.sum() == pytest.approx(1.0, abs=1e-6)
+    assert np.allclose(wx, wx[::-1]) and np.allclose(wy, wy[::-1])      # symmetric about the sited sample
+    assert wx[3] == wx.max() and wy[3] == wy[4] == wy.max()             # left-sited / centred
+    assert (wx[[0, 6]] < 0).all()                                        # C = 0.6 lobes
+
+
+def test_chroma_filter_changes_only_chroma(tm):
+    box = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2)
+    bic = box.with_(chroma_filter='bicubic')
+    a, _, _ = run_both(tm, box, 'uniform', 128, 64)
+    b, _, _ = run_both(tm, bic, 'uniform', 128, 64)
+    ysz = 128 * 64
+    assert np.array_equal(a[:, :ysz], b[:, :ysz])
+    assert not np.array_equal(a[:, ysz:], b[:, ysz:])
+
+
+# ---- S6 dither (App. B.4) and S8 expansion (App. B.6) -----------------------
+@pytest.mark.parametrize('bits_out', [8, 10, 12])
+@pytest.mark.parametrize('mode', ['compat8', 'native'])
+def test_ordered_dither_matches_oracle(tm, bits_out, mode):
+    params = hdr2sdr.TonemapParams(tonemapper='mobius', gamma=1.4, bits_out=bits_out, mode=mode, dither='ordered')
+    got, want, wh = run_both(tm, params, 'smooth', 128, 64)
+    assert_close_int(params, got, want, *wh)
+    plain, _, _ = run_both(tm, params.with_(dither='none'), 'smooth', 128, 64)
+    q = oracle.quant_bits(oracle.params_from(params.to_c()))
+    # swscale dithers only its 8-bit output: native 10/12-bit quantisers ignore it
+    assert np.array_equal(got, plain) == (q != 8)
+
+
+@pytest.mark.parametrize('bits_out', [10, 12])
+def test_bit_replication_matches_oracle(tm, bits_out):
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out, expand='replicate')
+    got, want, wh = run_both(tm, params, 'ramp', 128, 64)
+    assert_close_int(params, got, want, *wh)
+    s = bits_out - 8
+    v8 = got >> s
+    assert np.array_equal(got, (v8 << s) | (v8 >> (8 - s)))           # every code is a replication
+
+
+# ---- the libplacebo branch (src/utils.py:392-471) ---------------------------
+LP_CASES = {
+    'C3_bt2390': dict(tonemapper='bt.2390'),
+    'C3_bt2390_itu_knee': dict(tonemapper='bt.2390', knee_offset=0.5),
+    'bt2390_no_black': dict(tonemapper='bt.2390', target_black=0.0),
+    'spline': dict(tonemapper='spline'),
+    'spline_white100': dict(tonemapper='spline', target_white=100.0),
+    'bt2390_gamma13_eq': dict(tonemapper='bt.2390', gamma=1.3),
+    'bt2390_8bit': dict(tonemapper='bt.2390', bits_out=8),
+    'bt2390_hlg12': dict(tonemapper='bt.2390', bits_in=12, bits_out=12, transfer='arib-std-b67'),
+    'bt2390_lut_off_nv12': dict(tonemapper='bt.2390', lut_enabled=False),
+}
+
+
+@pytest.mark.parametrize('kind', ['smooth', 'uniform', 'ramp', 'edges'])
+@pytest.mark.parametrize('case', sorted(LP_CASES))
+def test_libplacebo_branch_matches_oracle(tm, case, kind):
+    params = hdr2sdr.TonemapParams(**LP_CASES[case])
+    assert params.resolved_pipeline() == 'libplacebo'
+    got, want, wh = run_both(tm, params, kind, 128, 64)
+    assert_close_int(params, got, want, *wh)
+
+
+def test_libplacebo_rgba_codes_use_the_full_output_depth(tm):
+    """The reference C3 output (rgba -> yuv420p10le, no eq at gamma 1) holds
+    10-bit codes that are not multiples of 4; the CPU chain's cannot."""
+    lp = hdr2sdr.TonemapParams(tonemapper='bt.2390')
+    cpu = lp.with_(pipeline='cpu')
+    a, _, _ = run_both(tm, lp, 'smooth', 128, 64)
+    b, _, _ = run_both(tm, cpu, 'smooth', 128, 64)
+    assert (a % 4 != 0).mean() > 0.5
+    assert (b % 4 == 0).all()
+    assert oracle.quant_bits(oracle.params_from(lp.to_c())) == 10
+    assert oracle.quant_bits(oracle.params_from(lp.with_(gamma=1.3).to_c())) == 8   # eq forces yuv420p
+
+
+def test_libplacebo_chain_string_selects_the_branch(tm):
+    chain = ('[0:v:0]format=p010,hwupload,libplacebo=w=iw:h=ih:tonemapping=bt.2390:colorspace=bt709:'
+             'color_primaries=auto:color_trc=bt709:range=tv:peak_detect=1:format=rgba,hwdownload,format=rgba,'
+             'lut3d=file=<LUT>:interp=tetrahedral,setparams=color_primaries=bt709:color_trc=bt709:'
+             'colorspace=bt709[vout]')
+    params, _ = hdr2sdr.parse_filter_chain(chain)
+    assert params.pipeline == 'libplacebo' and params.peak_detect
+    params = params.with_(peak_detect=False)
+    got, want, wh = run_both(tm, params, 'smooth', 128, 64)
+    assert_close_int(params, got, want, *wh)
+
+
+@pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])
+def test_libplacebo_dynamic_peak(W, H):
+    """peak_detect=1 (src/utils.py:448) on the libplacebo branch, across calls."""
+    from test_peak_detect import sequence
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
+    t = hdr2sdr.Tonemapper(0, params, lattice(65))
+    got = []
+    for a, b in ((0, 2), (2, 6)):
+        dst = hdr2sdr.FrameBatch.empty_numpy(b - a, W, H, 10)
+        t.process(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[a:b]), W, H, 10), dst)
+        got.append(dst.buf)
+    t.close()
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert_close_int(params, np.concatenate(got).astype(np.int64), want.astype(np.int64), W, H)
+
+
+# ---- the reference's second pixel gate --------------------------------------
+def identity_lattice(n):
+    g = np.linspace(0.0, 1.0, n, dtype=np.float64)
+    b, gg, r = np.meshgrid(g, g, g, indexing='ij')           # .cube order: red fastest
+    return np.stack([r.ravel(), gg.ravel(), b.ravel()], axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize('kind,seed', [('smooth', 21), ('ramp', 5)])
+def test_gpu_lut_stage_changes_hable_output(kind, seed):
+    """TestGpuLutStageActuallyChangesCpuCapableTonemapperOutput
+    (test/smoke_test.py:386-435) on the product path: Hable, one 960x540
+    HDR10 frame rendered as the reference's preview PNG, with the LUT stage
+    vs with that stage a no-op (an identity lattice: the failure the gate
+    guards against, "the LUT stage has silently become a no-op"), sampled on
+    the 21 x 21 grid (w // 20 steps): the max per-channel difference must be
+    >= 30/255 (_MIN_EXPECTED_DIFF, :408).  The reference measured ~61/255
+    against libplacebo's own gamut mapping, which is not restated here."""
+    from hdr2sdr import preview as PV
+    W, H = 960, 540
+    src = synth_frames(kind, 1, W, H, 10, device='cpu', seed=seed).to_numpy()
+    imgs = []
+    for lat in (lattice(65), identity_lattice(65)):
+        with PV.Previewer(0, tonemapper='hable', lut_enabled=True, lattice=lat) as pv:
+            imgs.append(pv.convert(src, 'iw', 'ih').astype(int))
+    xs = np.arange(0, W, max(1, W // 20))
+    ys = np.arange(0, H, max(1, H // 20))
+    d = np.abs(imgs[0][ys][:, xs] - imgs[1][ys][:, xs])
+    assert d.max() >= 30, f'LUT stage changes the Hable output by only {d.max()}/255'

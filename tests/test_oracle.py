@@ -71,12 +71,59 @@ def test_tone_curve_known_answers():
     assert ys[0] < 1e-3 and all(b >= a for a, b in zip(ys, ys[1:]))
 
 
-def test_bt2390_eetf_shape():
-    p = params(tonemap='bt.2390')
+PIPE_CPU, PIPE_LP = 1, 2
+
+
+@pytest.mark.parametrize('knee', [0.5, 1.0])
+def test_bt2390_eetf_shape(knee):
+    """CPU-chain target (npl white, no black): identity below the knee, the
+    source peak onto the target white, clipped above the source range."""
+    p = params(tonemap='bt.2390', pipeline=PIPE_CPU, knee_offset=knee)
     assert oracle.tone_curve(p, 0.01) == pytest.approx(0.01, rel=1e-3)     # below the knee: identity
     top = oracle.tone_curve(p, 10.0)                                        # source peak -> target peak
     assert top == pytest.approx(1.0, rel=1e-3)
     assert oracle.tone_curve(p, 100.0) == pytest.approx(top, rel=1e-6)      # clipped to source range
+
+
+def _bt2390_ref(sig, peak=10.0, white=203.0, black=0.203, offset=1.0):
+    """Independent double transcription of libplacebo's bt2390 (knee offset,
+    black-point adaptation); sig in units of 100 nits, output in units of the
+    target white."""
+    smin, smax = _pq_enc(0.0), _pq_enc(peak / 100.0)
+    ml = (_pq_enc(white / 10000.0) - smin) / (smax - smin)
+    mn = (_pq_enc(black / 10000.0) - smin) / (smax - smin) if black > 0 else 0.0
+    ks = (1 + offset) * ml - offset
+    bp = min(1 / mn, 4.0) if mn > 0 else 4.0
+    gain = 1 / (1 + mn / ml * (1 - ml) ** bp) if ml < 1 else 1.0
+    x = min(max((_pq_enc(sig / 100.0) - smin) / (smax - smin), 0.0), 1.0)
+    if ks < 1 and x > ks:
+        t = (x - ks) / (1 - ks)
+        x = (2 * t ** 3 - 3 * t ** 2 + 1) * ks + (t ** 3 - 2 * t ** 2 + t) * (1 - ks) + (-2 * t ** 3 + 3 * t ** 2) * ml
+    if mn > 0 and x < 1:
+        x += mn * (1 - x) ** bp
+        x = gain * (x - mn) + mn
+    return oracle.pq_eotf_d(x * (smax - smin) + smin) * 10000.0 / white
+
+
+@pytest.mark.parametrize('peak,knee,black', [(10.0, 1.0, None), (40.0, 1.0, None), (10.0, 0.5, None),
+                                             (10.0, 1.0, 0.0), (4.0, 2.0, 1.0)])
+def test_bt2390_libplacebo_matches_independent_transcription(peak, knee, black):
+    """libplacebo branch defaults: 203-nit white, 1000:1 black, knee offset 1."""
+    kw = dict(tonemap='bt.2390', pipeline=PIPE_LP, peak=peak, knee_offset=knee)
+    if black is not None:
+        kw['target_black'] = black
+    p = params(**kw)
+    for sig in (1e-4, 0.003, 0.05, 0.2, 0.5, 1.0, 2.0, 5.0, peak * 0.7, peak):
+        want = _bt2390_ref(sig, peak=peak, offset=knee, black=0.203 if black is None else black)
+        assert oracle.tone_curve(p, sig) == pytest.approx(want, rel=5e-4, abs=1e-6), sig
+
+
+def test_bt2390_black_point_lifts_black():
+    p = params(tonemap='bt.2390', pipeline=PIPE_LP)
+    # black maps onto the target black (0.203 of 203 nits = 1e-3 of white)
+    assert oracle.tone_curve(p, 1e-6) == pytest.approx(1e-3, rel=5e-2)
+    off = params(tonemap='bt.2390', pipeline=PIPE_LP, target_black=0.0)
+    assert oracle.tone_curve(off, 1e-6) < 1e-6
 
 
 # ---- libplacebo spline (PARITY UNPINNED: libplacebo absent) ----------------
@@ -86,14 +133,16 @@ def _pq_enc(y):
     return ((c1 + c2 * ym) / (1 + c3 * ym)) ** m2
 
 
-def _spline_ref(sig, peak=10.0, npl=100.0, contrast=0.5, avg_pq=0.0):
+def _spline_ref(sig, peak=10.0, npl=100.0, contrast=0.5, avg_pq=0.0, black=0.0, white=None):
     """Second, independent transcription of libplacebo's spline (pick_knee +
-    single-pivot toe/shoulder, tone_mapping.c defaults) in double."""
+    single-pivot toe/shoulder, tone_mapping.c defaults) in double; output in
+    units of the target white (default npl)."""
     def smoothstep(e0, e1, x):
         t = min(max((x - e0) / (e1 - e0), 0.0), 1.0)
         return t * t * (3 - 2 * t)
+    white = npl if white is None else white
     smin, smax = _pq_enc(0.0), _pq_enc(peak / 100.0)
-    dmin, dmax = _pq_enc(0.0), _pq_enc(npl / 10000.0)
+    dmin, dmax = _pq_enc(black / 10000.0), _pq_enc(white / 10000.0)
     sk = avg_pq if avg_pq > 0 else smin + 0.4 * (smax - smin)
     sk = min(max(sk, smin + 0.1 * (smax - smin)), smin + 0.8 * (smax - smin))
     target = (sk - smin) / (smax - smin)
@@ -109,19 +158,21 @@ def _spline_ref(sig, peak=10.0, npl=100.0, contrast=0.5, avg_pq=0.0):
     else:
         y = ((o0 - slope * i0) / (i0 * i0) * x + slope) * x
     e2 = min(max(y + dk, dmin), dmax)
-    return oracle.pq_eotf_d(e2) * 10000.0 / npl, sk, dk, slope
+    return oracle.pq_eotf_d(e2) * 10000.0 / white, sk, dk, slope
 
 
 @pytest.mark.parametrize('peak,contrast', [(10.0, 0.5), (40.0, 0.5), (10.0, 0.0), (10.0, 1.5), (2.0, 0.5)])
-def test_spline_matches_independent_transcription(peak, contrast):
-    p = params(tonemap='spline', peak=peak, tm_param=contrast)
+@pytest.mark.parametrize('pipe', [PIPE_CPU, PIPE_LP])
+def test_spline_matches_independent_transcription(peak, contrast, pipe):
+    p = params(tonemap='spline', peak=peak, tm_param=contrast, pipeline=pipe)
+    tgt = dict(black=0.203, white=203.0) if pipe == PIPE_LP else {}
     for sig in (1e-4, 0.003, 0.05, 0.2, 0.5, 1.0, 2.0, 5.0, peak * 0.7, peak, peak * 3):
-        want = _spline_ref(sig, peak=peak, contrast=contrast)[0]
+        want = _spline_ref(sig, peak=peak, contrast=contrast, **tgt)[0]
         assert oracle.tone_curve(p, sig) == pytest.approx(want, rel=2e-4, abs=1e-6), sig
 
 
 def test_spline_shape():
-    p = params(tonemap='spline')                     # peak 10 (1000 nits), contrast 0.5
+    p = params(tonemap='spline', pipeline=PIPE_CPU)  # peak 10 (1000 nits), contrast 0.5
     xs = np.geomspace(1e-4, 10.0, 300)
     ys = [oracle.tone_curve(p, float(x)) for x in xs]
     assert all(b >= a - 1e-7 for a, b in zip(ys, ys[1:]))               # monotone

@@ -71,12 +71,13 @@ def sequence(W=256, H=128):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('pipeline', ['cpu', 'libplacebo'])  # cpu: the tile kernel's per-frame curve records
 @pytest.mark.parametrize('tmname', ['bt.2390', 'spline'])   # spline also takes its knee from the average
 @pytest.mark.parametrize('W,H', [(256, 128), (192, 96), (200, 96)])   # fast path (blocks within / across frames), + tail
-def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname):
+def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline):
     from test_gpu_parity import assert_close_int, lattice
     buf = sequence(W, H)
-    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0, pipeline=pipeline)
     tm = hdr2sdr.Tonemapper(0, params, lattice(65))
     got = []
     for a, b in ((0, 2), (2, 5), (5, 6)):            # the state carries across calls
@@ -120,7 +121,7 @@ def test_gpu_dynamic_peak_hlg12(W, H):
     from test_gpu_parity import assert_close_int, lattice
     buf = synth_frames('smooth', 4, W, H, 12, device='cpu', seed=77).to_numpy().buf
     params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, transfer='arib-std-b67',
-                                   bits_in=12, bits_out=12)
+                                   bits_in=12, bits_out=12, pipeline='cpu')
     tm = hdr2sdr.Tonemapper(0, params, lattice(65))
     src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 12)
     dst = hdr2sdr.FrameBatch.empty_numpy(4, W, H, 12)
