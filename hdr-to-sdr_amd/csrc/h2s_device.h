@@ -144,6 +144,11 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 // x^p for x >= 0 (x == 0 -> 0 for p > 0)
 __device__ __forceinline__ float fpow(float x, float p) { return fexp2(p * flog2(x)); }
+// the generic chain's pow: ocml powf (faithfully rounded, as libm's powf in
+// the oracle).  The PQ exponents amplify a v_log/v_exp ulp ~100-fold
+// (m2 = 78.84; the xp - c1 cancellation), enough to flip the libplacebo
+// branch's 8-bit rgba rounding; the tile kernel keeps its own fast forms
+__device__ __forceinline__ float apow(float x, float p) { return powf(x, p); }
 __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
 
 // ST 2084 constants (exact binary values, as zimg defines them)
@@ -159,29 +164,29 @@ __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed
 // S1 transfer: zimg st_2084_eotf (normalised, 1.0 = 10000 nits)
 __device__ __forceinline__ float pq_eotf(float x) {
   if (!(x > 0.0f)) return 0.0f;
-  float xpow = fpow(x, 1.0f / PQ_M2);
+  float xpow = apow(x, 1.0f / PQ_M2);
   float num = fmaxf(xpow - PQ_C1, 0.0f);
   float den = fmaxf(PQ_C2 - PQ_C3 * xpow, 1.17549435e-38f);
-  return fpow(num * frcp(den), 1.0f / PQ_M1);
+  return apow(num / den, 1.0f / PQ_M1);
 }
 
 // ST 2084 inverse EOTF (BT.2390 works in the PQ domain)
 __device__ __forceinline__ float pq_encode(float y) {
-  float ym = fpow(fmaxf(y, 0.0f), PQ_M1);
-  return fpow((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym), PQ_M2);
+  float ym = apow(fmaxf(y, 0.0f), PQ_M1);
+  return apow((PQ_C1 + PQ_C2 * ym) / (1.0f + PQ_C3 * ym), PQ_M2);
 }
 
 // zimg arib_b67_inverse_oetf
 __device__ __forceinline__ float hlg_inv_oetf(float x) {
   x = fmaxf(x, 0.0f);
   if (x <= 0.5f) return (x * x) * (1.0f / 3.0f);
-  return (fexp2((x - HLG_C) * (1.0f / HLG_A) * 1.44269504f) + HLG_B) * (1.0f / 12.0f);
+  return (expf((x - HLG_C) / HLG_A) + HLG_B) * (1.0f / 12.0f);
 }
 
 // vf_tonemap hable()
 __device__ __forceinline__ float hable(float in) {
   const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
-  return (in * (in * a + b * c) + d * e) * frcp(in * (in * a + b) + d * f) - e / f;
+  return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
 }
 
 // libplacebo spline on a PQ-domain signal: quadratic toe below the knee,
@@ -198,7 +203,7 @@ __device__ __forceinline__ float spline_pq(const K& P, float e) {
 __device__ __forceinline__ float bt2390_black(float mn, float bp, float gain, float x) {
   if (!(mn > 0.0f) || !(x < 1.0f)) return x;
   const float om = 1.0f - x;
-  const float pw = bp == 4.0f ? (om * om) * (om * om) : fpow(om, bp);
+  const float pw = bp == 4.0f ? (om * om) * (om * om) : apow(om, bp);
   x += mn * pw;
   return gain * (x - mn) + mn;
 }
@@ -209,7 +214,7 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
   if (P.tonemap == 8 /* SPLINE */) {
     sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     const float s2 = pq_eotf(spline_pq(P, pq_encode(sig * P.npl_1e4))) * P.e4_npl;
-    const float k = s2 * frcp(sig);
+    const float k = s2 / sig;
     r *= k, g *= k, b *= k;
     return;
   }
@@ -226,13 +231,13 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
     }
     e2 = bt2390_black(P.b_minlum, P.b_bp, P.b_gain, e2);
     float s2 = pq_eotf(e2 * P.b_range + P.b_srcmin) * P.e4_npl;
-    float k = s2 * frcp(sig);
+    float k = s2 / sig;
     r *= k, g *= k, b *= k;
     return;
   }
   if (P.desat_on) {
     float luma = P.lr * r + P.lg * g + P.lb * b;
-    float ob = fmaxf(luma - P.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
+    float ob = fmaxf(luma - P.desat, 1e-6f) / fmaxf(luma, 1e-6f);
     r = r * (1.0f - ob) + luma * ob;
     g = g * (1.0f - ob) + luma * ob;
     b = b * (1.0f - ob) + luma * ob;
@@ -244,30 +249,30 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
       sig = sig * P.lin_k;
       break;
     case 2:  // GAMMA
-      sig = sig > 0.05f ? fpow(sig * P.gam_inv_peak, P.gam_inv_param) : sig * P.gam_low_k;
+      sig = sig > 0.05f ? apow(sig * P.gam_inv_peak, P.gam_inv_param) : sig * P.gam_low_k;
       break;
     case 3:  // CLIP
       sig = clamp01(sig * P.clip_k);
       break;
     case 4:  // REINHARD
-      sig = sig * frcp(sig + P.rein_p) * P.rein_k;
+      sig = sig / (sig + P.rein_p) * P.rein_k;
       break;
     case 5:  // HABLE
       sig = hable(sig) * P.hable_peak_inv;
       break;
     case 6:  // MOBIUS
-      sig = sig <= P.mob_j ? sig : P.mob_k * (sig + P.mob_a) * frcp(sig + P.mob_b);
+      sig = sig <= P.mob_j ? sig : P.mob_k * (sig + P.mob_a) / (sig + P.mob_b);
       break;
     default:
       break;
   }
-  float k = sig * frcp(sig_orig);
+  float k = sig / sig_orig;
   r *= k, g *= k, b *= k;
 }
 
 // S3: zimg rec_1886_inverse_eotf
 __device__ __forceinline__ float bt1886_inv(float x) {
-  return x > 0.0f ? fpow(x, 1.0f / 2.4f) : 0.0f;
+  return x > 0.0f ? apow(x, 1.0f / 2.4f) : 0.0f;
 }
 
 // S4: vf_lut3d sanitizef + clip + interp_tetrahedral.  The lattice is in
@@ -314,7 +319,7 @@ __device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g
 // libplacebo branch: BT.1886 encode against the target black (oracle lp_encode)
 __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
   x = x > 0.0f ? x : 0.0f;
-  return fpow(x * P.enc_ainv, 1.0f / 2.4f) - P.enc_b;
+  return apow(x * P.enc_ainv, 1.0f / 2.4f) - P.enc_b;
 }
 
 // libplacebo branch: rgba8 download (round to nearest), then vf_lut3d's 8-bit
@@ -344,7 +349,7 @@ __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, fl
   if (P.transfer == 1) {  // HLG: inverse OETF + OOTF (gamma 1.2 at 1000 nits)
     r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), b = hlg_inv_oetf(eb);
     float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
-    float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
+    float w = ys > 0.0f ? P.lin_scale * apow(ys, 0.2f) : 0.0f;
     r *= w, g *= w, b *= w;
   } else {
     r = pq_eotf(er) * P.lin_scale;

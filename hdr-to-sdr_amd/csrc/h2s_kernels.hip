@@ -341,7 +341,7 @@ __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned
   if (TRC == 0) return clamp01(fmaxf(fmaxf(er, eg), eb));
   const float r = hlg_inv_oetf(er), g = hlg_inv_oetf(eg), bl = hlg_inv_oetf(eb);
   const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * bl;
-  const float w = ys > 0.0f ? P.lin_scale * fpow(ys, 0.2f) : 0.0f;
+  const float w = ys > 0.0f ? P.lin_scale * apow(ys, 0.2f) : 0.0f;
   return clamp01(pq_encode(fmaxf(fmaxf(r, g), bl) * w * P.npl_1e4));
 }
 

@@ -1,0 +1,78 @@
+"""Diagnostics for GPU-vs-oracle mismatches (prints distributions, worst
+entries).  Usage on the GPU box: python scripts/diag_parity.py"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, 'hdr-to-sdr_amd'), REPO, os.path.join(REPO, 'tests')]
+import oracle  # noqa: E402
+import hdr2sdr  # noqa: E402
+from hdr2sdr import _abi  # noqa: E402
+from hdr2sdr.synth import synth_frames  # noqa: E402
+
+LAT = hdr2sdr.generate_lattice(65)
+
+
+def int_case(tm, kw, kind, W=128, H=64):
+    import torch
+    p = hdr2sdr.TonemapParams(**kw)
+    src = synth_frames(kind, 2, W, H, p.bits_in, device='cpu', seed=11)
+    tm.set_params(p)
+    tm.set_lut(LAT)
+    dst = hdr2sdr.FrameBatch.empty_torch(2, W, H, p.bits_out, 'cuda')
+    tm.process(src.to_torch('cuda'), dst)
+    torch.cuda.synchronize()
+    got = dst.to_numpy().buf.astype(np.int64)
+    want = oracle.process(oracle.params_from(p.to_c()), LAT, src.to_numpy().buf, W, H).astype(np.int64)
+    d = np.abs(got - want)
+    vals, cnt = np.unique(d, return_counts=True)
+    print(f'{kw} {kind}: differing {float((d > 0).mean()):.4%}, hist {dict(zip(vals.tolist(), cnt.tolist()))}')
+    for st in (2, 3, 4, 5):
+        g = tm.debug_float(src.to_torch('cuda'), st).astype(np.float64)
+        w = oracle.debug_float(oracle.params_from(p.to_c()), LAT, src.to_numpy().buf, W, H, st).astype(np.float64)
+        e = np.abs(g - w)
+        e[np.isnan(e) & np.isnan(w)] = 0
+        i = np.unravel_index(np.nanargmax(e), e.shape)
+        print(f'   stage {st}: max abs err {np.nanmax(e):.3g} at want {w[i]:.6g} got {g[i]:.6g}; '
+              f'rel>1e-3: {int((e > 1e-3 * np.abs(w) + 1e-7).sum())}')
+
+
+def float_case(tm, kw, kind, stage, fast, W=128, H=64):
+    p = hdr2sdr.TonemapParams(**kw)
+    src = synth_frames(kind, 1, W, H, p.bits_in, device='cpu', seed=3)
+    tm.set_params(p)
+    tm.set_lut(LAT)
+    tm.set_option(_abi.OPT_FAST_PATH, fast)
+    g = tm.debug_float(src.to_torch('cuda'), stage).astype(np.float64)
+    tm.set_option(_abi.OPT_FAST_PATH, 1)
+    w = oracle.debug_float(oracle.params_from(p.to_c()), LAT, src.to_numpy().buf, W, H, stage).astype(np.float64)
+    e = np.abs(g - w)
+    tol = 1e-3 * np.abs(w) + 2e-7
+    r = e / tol
+    r[np.isnan(r)] = 0
+    order = np.argsort(r.ravel())[::-1][:4]
+    print(f'{kw} {kind} stage {stage} fast {fast}:')
+    for o in order:
+        c, y, x = np.unravel_index(o, w.shape)
+        # the pixel's linear inputs (stage 1) for context
+        print(f'   [{c},{y},{x}] want {w[c, y, x]:.9g} got {g[c, y, x]:.9g} err/tol {r[c, y, x]:.3g}')
+
+
+if __name__ == '__main__':
+    tm = hdr2sdr.Tonemapper(0)
+    for kw, kind in ((dict(tonemapper='bt.2390'), 'smooth'), (dict(tonemapper='bt.2390', knee_offset=0.5), 'uniform'),
+                     (dict(tonemapper='bt.2390', bits_in=12, bits_out=12, transfer='arib-std-b67'), 'smooth'),
+                     (dict(tonemapper='spline', target_white=100.0), 'smooth'),
+                     (dict(tonemapper='spline', bits_in=12, bits_out=12, transfer='arib-std-b67', tm_param=1.0,
+                           pipeline='cpu'), 'smooth'),
+                     (dict(tonemapper='bt.2390', pipeline='cpu', mode='native'), 'smooth')):
+        int_case(tm, kw, kind)
+    for kw, kind, st, fast in ((dict(tonemapper='hable', gamma=2.2, bits_out=10), 'uniform', 2, 0),
+                               (dict(tonemapper='hable', gamma=2.2, bits_out=10), 'uniform', 3, 1),
+                               (dict(tonemapper='hable', gamma=2.2, bits_out=10), 'edges', 2, 0),
+                               (dict(tonemapper='mobius', bits_out=10, mode='native'), 'uniform', 2, 0),
+                               (dict(tonemapper='mobius', bits_out=10, mode='native'), 'uniform', 3, 0)):
+        float_case(tm, kw, kind, st, fast)
+    tm.close()

@@ -54,22 +54,32 @@ def run_both(tm, params, kind, W, H, nframes=2, lut_n=65, seed=11):
     return got, want, (W, H)
 
 
-def assert_close_int(params, got, want, W, H, max_frac=5e-3):
+def _lattice_max_step(n):
+    a = lattice(n).reshape(n, n, n, 3).astype(np.float64)
+    return max(float(np.abs(np.diff(a, axis=ax)).max()) for ax in range(3))
+
+
+def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
     """Chroma: |diff| <= one quantisation step.  Luma: eq runs after the
     quantiser, so the bound is +-1 step *before* eq: got must lie between
     eq[q-1] and eq[q+1] where eq[q] == want (eq is monotonic).
 
     The libplacebo branch quantises twice before the output (the 8-bit rgba
-    download and lut3d's truncating 8-bit output): a float-rounding flip there
-    moves one R'G'B' channel by 1/255, i.e. Y'CbCr at depth q by at most
-    ceil(224 * 2^(q-8) / 255) + 1 steps — that is its bound."""
+    download and lut3d's truncating 8-bit output).  A float-rounding flip of
+    the download moves the lattice coordinate by (N-1)/255 cells, i.e. the
+    LUT output by up to D (N-1) 8-bit steps, D the largest difference between
+    neighbouring lattice points (steep near black, where the gamut clip
+    bends), plus one for the truncation; through the BT.709 rows that is
+    Y'CbCr at depth q.  That is its bound, and at most max_frac of the
+    samples may sit more than one output step off."""
     op = oracle.params_from(params.to_c())
     q = oracle.quant_bits(op)
     if params.resolved_pipeline() == 'libplacebo' and params.lut_enabled:
         step = 1 << (params.bits_out - q)
-        bound = (-(-224 * (1 << (q - 8)) // 255) + 1) * step
+        k8 = math.ceil(_lattice_max_step(lut_n) * (lut_n - 1)) + 1
+        bound = (math.ceil(k8 * 224 * (1 << (q - 8)) / 255) + 1) * step
         d = np.abs(got - want)
-        assert d.max(initial=0) <= bound, f'max diff {d.max()} > {bound} (one 8-bit R\'G\'B\' step)'
+        assert d.max(initial=0) <= bound, f'max diff {d.max()} > {bound} ({k8} 8-bit R\'G\'B\' steps)'
         frac = float((d > step).mean())
         assert frac <= max_frac, f'{frac:.3%} of samples beyond one step'
         return
@@ -229,11 +239,37 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
         want = np.clip(want, 0.0, 1.0)      # k_tile clamps x to [0, 1) before the power (lattice coordinate)
     q = oracle.quant_bits(op)
     floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
-    err = np.abs(got.astype(np.float64) - want)
+    got = got.astype(np.float64)
+    with np.errstate(invalid='ignore'):
+        err = np.abs(got - want)
+    # Two places where the reference's own float32 chain is ill-conditioned,
+    # excluded and counted (< 1 % of uniform / ramp frames; 9 % of 'edges',
+    # which puts a third of its codes in the out-of-range bands; none in the
+    # range real content occupies):
+    # * the ST 2084 pole: codes whose E' reaches ~1.9 (super-white Y' with
+    #   extreme chroma) make c2 - c3 E'^(1/m2) cancel; linear > 1e6 x npl;
+    # * vf_tonemap's desat kink: (luma - desat) cancels.  The PQ EOTF in
+    #   float32 amplifies one ulp of its pow ~80-fold (xp - c1, then ^6.28),
+    #   so any two implementations differ by ~1e-5 relative at stage 1, i.e.
+    #   by 1e-5 luma / |luma - desat| relative at stage 2: excluded where that
+    #   exceeds half the 1e-3 budget, |luma - desat| < 0.02 luma.
+    lin = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 1).astype(np.float64)
+    skip = ~(np.nanmax(np.abs(np.nan_to_num(lin, nan=np.inf)), axis=0) < 1e6)
+    if stage >= 2 and params.desat > 0 and params.tonemapper not in ('bt.2390', 'spline'):
+        wts = {'rgb': (1, 1, 1), 'bt2020': (0.2627, 0.6780, 0.0593), 'bt709': (0.2126, 0.7152, 0.0722)}
+        lr, lg, lb = wts[params.desat_luma]
+        with np.errstate(invalid='ignore'):
+            luma = lr * lin[0] + lg * lin[1] + lb * lin[2]
+            skip |= np.abs(luma - params.desat) < 0.02 * luma
+    assert skip.mean() < (0.1 if kind == 'edges' else 0.01)
+    keep = np.broadcast_to(~skip[None], want.shape)
+    assert np.isfinite(want[keep]).all() and np.isfinite(got[keep]).all()
     tol = 1e-3 * np.abs(want) + floor
-    bad = err > tol
-    assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {floor:g}; '
-                           f'worst err {float(err.max()):.3g} at want {float(want.flat[int(err.argmax())]):.4g}')
+    bad = (err > tol) & keep
+    i = int(np.argmax(np.where(bad, err / tol, 0)))
+    assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {floor:g} '
+                           f'({int(skip.sum())} ill-conditioned pixels excluded); worst: want '
+                           f'{float(want.flat[i]):.6g} got {float(got.flat[i]):.6g}')
 
 
 def test_host_memory_path_equals_device_path(tm):
