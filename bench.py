@@ -76,7 +76,8 @@ def launch_ranks(gpus: int) -> int:
 
 def cpu_baseline(params, lattice, width, height, budget_s):
     """Oracle (C restatement of the reference chain, OpenMP) on the host
-    cores, on a bounded sample: whole frames until ~budget_s elapse."""
+    cores, on a bounded sample: whole frames until ~budget_s elapse, on all
+    allowed host threads and on 1 thread (BASELINE.md's CPU plan)."""
     import numpy as np
     import oracle
     from hdr2sdr.synth import synth_frames
@@ -88,18 +89,25 @@ def cpu_baseline(params, lattice, width, height, budget_s):
     p = oracle.params_from(params.to_c())
     src = synth_frames('smooth', 1, width, height, params.bits_in, device='cpu', seed=0x5EED).to_numpy()
     buf = np.ascontiguousarray(src.buf)
-    oracle.process(p, lattice, buf, width, height, nthreads=cores)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle.process(p, lattice, buf, width, height, nthreads=cores)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 1024:
-            break
+
+    def rate(nthreads, budget):
+        oracle.process(p, lattice, buf, width, height, nthreads=nthreads)  # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            oracle.process(p, lattice, buf, width, height, nthreads=nthreads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 1024:
+                return n, el
+
+    n, el = rate(cores, budget_s * 2 / 3)
+    n1, el1 = rate(1, budget_s / 3)
     mpx = n * width * height / el / 1e6
     return {'value': round(mpx, 3), 'unit': 'Mpixel/s', 'cores': cores, 'kind': 'port',
-            'sample': f'{n} x {width}x{height} smooth frame(s), same chain/params, {el:.1f} s, '
-                      f'oracle/h2s_oracle.c (C restatement of the ffmpeg chain, not ffmpeg) with {cores} OpenMP threads'}
+            'value_1thread': round(n1 * width * height / el1 / 1e6, 3),
+            'sample': f'{n} x {width}x{height} smooth frame(s) in {el:.1f} s on {cores} OpenMP threads, '
+                      f'{n1} in {el1:.1f} s on 1 thread (value_1thread); same chain/params; '
+                      f'oracle/h2s_oracle.c (C restatement of the ffmpeg chain, not ffmpeg)'}
 
 
 def pmc_traffic(workload):
@@ -268,7 +276,9 @@ def main():
         other = {}
         for tag, kw, w_, h_, nf, lut_n in (
                 ('C1', dict(tonemapper='reinhard', gamma=1.0, bits_out=8), 1920, 1080, 16, 33),
+                # C3 as the reference runs it: the libplacebo branch (rgba8 + lut3d 8-bit, src/utils.py:444-460)
                 ('C3', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
+                ('C3_cpu_chain', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, pipeline='cpu'), 3840, 2160, 16, 65),
                 ('C4', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 ('C5', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
                  7680, 4320, 4, 65),
@@ -325,7 +335,8 @@ def main():
         'data': 'synthetic',
         'config': {
             'workload': (f'C2: {W}x{H} PQ HDR10 yuv420p{args.bits_in}le -> yuv420p{args.bits_out}le, '
-                         f'{args.tonemapper} + {n}^3 tetrahedral LUT + eq gamma {args.gamma}, mode {args.mode}'),
+                         f'{args.tonemapper} + {n}^3 tetrahedral LUT + eq gamma {args.gamma}, mode {args.mode}, '
+                         f'{B} frames per launch'),
             'frames_per_rank_per_step': B,
             'width': W, 'height': H,
             'content': args.kind,

@@ -17,7 +17,7 @@ namespace h2s {
 hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
 hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
 bool fast_supported(int tonemap);
-hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s, int dbg = 0);
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg = 0);
 hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
@@ -47,6 +47,7 @@ struct h2s_ctx {
   int lut_n = 0;
   float* d_lut_yuv = nullptr;  // lattice pre-multiplied into output code space (3 floats/point)
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
+  int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   bool fast_enabled = true;
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
@@ -676,6 +677,11 @@ static void curve_fast(const KParams& k, h2s::CurveConsts* cc) {
     cc->sp_pa_u = (float)(seg * k.sp_pa), cc->sp_pb_u = (float)(seg * k.sp_pb);
     cc->sp_k_u = (float)(seg * k.sp_kout + 1.0);
     cc->sp_umin = (float)(seg * k.sp_dmin + 1.0), cc->sp_umax = (float)(seg * k.sp_dmax + 1.0);
+    // black-point adaptation in u: 1 - e2 = (R + C - u) / R; u' = gain u +
+    // R gain mn (1 - e2)^bp + (1 - gain)(C + R mn)   (e2 < 1)
+    const double mn = k.b_minlum, gain = k.b_gain;
+    cc->b_bk_a = (float)(-1.0 / R), cc->b_bk_b = (float)((R + C) / R);
+    cc->b_bk_c = (float)(R * gain * mn), cc->b_bk_d = (float)((1.0 - gain) * (C + R * mn));
   }
 }
 
@@ -712,6 +718,16 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->mob_j = k.mob_j, F->mob_a = k.mob_a, F->mob_b = k.mob_b, F->mob_k = k.mob_k;
   F->npl_1e4 = k.npl_1e4, F->e4_npl = k.e4_npl;
   F->b_e1min = (float)pq_encode_d(1e-6 * p->npl / 10000.0);
+  F->tw_fold = (float)(p->npl / k.t_white);
+  // libplacebo branch: 255 ((x ainv)^(1/2.4) - b) as exp2(log2(x)/2.4 + k1) - k2
+  F->lp_k1 = (float)(log2((double)k.enc_ainv) / 2.4 + log2(255.0));
+  F->lp_k2 = (float)(255.0 * (double)k.enc_b);
+  F->lp_xmax = (float)(pow(1.0 + (double)k.enc_b, 2.4) / (double)k.enc_ainv * 1.001);
+  F->nm1 = (float)(c->lut_n - 1);
+  F->inv255 = 1.0f / 255.0f;
+  F->qscale = k.qscale;
+  F->c56 = 56.0f * k.qscale;
+  for (int i = 0; i < 3; i++) F->k709[i] = k.k709[i], F->kcb[i] = k.kcb[i], F->kcr[i] = k.kcr[i];
   curve_fast(k, F);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
@@ -736,7 +752,7 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
 }
 
 static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
-  if (c->d_lut_yuv && c->lut_yuv_scale == k.qscale) return 0;
+  if (c->d_lut_yuv && c->lut_yuv_scale == k.qscale && c->lut_yuv_rgb == k.rgba8) return 0;
   const size_t cnt = (size_t)c->lut_n * c->lut_n * c->lut_n;
   if (!c->d_lut_yuv) {
     const size_t m = (size_t)c->lut_n - 1;
@@ -749,10 +765,12 @@ static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
   }
   h2s::YuvLutConsts K;
   K.s = k.qscale;
+  K.rgb = k.rgba8;
   for (int i = 0; i < 3; i++) K.k709[i] = k.k709[i], K.kcb[i] = k.kcb[i], K.kcr[i] = k.kcr[i];
   hipError_t e = h2s::build_lut_yuv(c->d_lut, c->d_lut_yuv, c->lut_n, K, s);
   if (e != hipSuccess) return hip_fail(c, e, "YUV lattice build");
   c->lut_yuv_scale = k.qscale;
+  c->lut_yuv_rgb = k.rgba8;
   return 0;
 }
 
@@ -854,13 +872,13 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.dbg_lut = c->d_lut;
   F.inv_nm1 = 1.0f / (float)(c->lut_n - 1);
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
-  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, s, dbg);
+  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.rgba8, s, dbg);
   if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
   return launch_tail(k, nframes, vec, out8, s);
 }
 
-// the tile kernel serves: the CPU chain (the libplacebo branch's rgba8 /
-// target / black-point stages run on the generic kernel), the LUT on at
+// the tile kernel serves: both of the reference's chains (the CPU chain, and
+// the libplacebo branch with the LUT on: k_tile<..., LP = 1>), the LUT on at
 // N <= 177 (its lattice byte offsets are formed in float32, exact for
 // multiples of 4 below 2^26 = 12 * 177^3 + margin), the default [EXT]
 // switches, 10/12-bit input and BASELINE's operators; frames with a 64-wide
@@ -869,11 +887,7 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   const h2s_params& p = c->params;
   if (!c->fast_enabled || !k.lut_enabled || !h2s::fast_supported(k.tonemap)) return false;
   if (c->lut_n > 177) return false;
-  if (k.pipe != h2s::PIPE_CPU) return false;
   if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out)) return false;
-  if ((k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE) &&
-      (k.b_minlum != 0.0f || k.t_white != p.npl))
-    return false;  // the folded curve decodes through the npl-scaled EOTF table
   return true;
 }
 

@@ -80,6 +80,9 @@ struct CurveConsts {
   float sp_srcmin, sp_srcmax, sp_kin, sp_kout, sp_pa, sp_pb, sp_qa, sp_qb, sp_qc, sp_dmin, sp_dmax;  // SPLINE
   // spline: u = Horner(x) with the coefficients and kout scaled by PQ_SEG, clamped to [umin, umax]
   float sp_qa_u, sp_qb_u, sp_qc_u, sp_pa_u, sp_pb_u, sp_k_u, sp_umin, sp_umax;
+  // BT.2390 black-point adaptation on the table coordinate u = e2*R + C:
+  // 1 - e2 = u*bk_a + bk_b; u' = gain*u + bk_c*(1 - e2)^bp + bk_d for e2 < 1
+  float b_bk_a, b_bk_b, b_bk_c, b_bk_d;
 };
 
 // Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
@@ -105,7 +108,13 @@ struct FastParams : CurveConsts {
   float hable_ka, hable_kb;        // 0.14 / hable(peak), (1/60) / hable(peak): hable(x)/x = (0.14 x + 1/60) / D(x)
   float mob_j, mob_a, mob_b, mob_k;
   float npl_1e4, e4_npl;
+  float tw_fold;                   // BT.2390 / spline on PQ input: npl / target white (the EOTF table is npl-scaled)
   float b_e1min;                   // PQ code of sig = 1e-6 (BT.2390 / spline e1 lower bound)
+  // libplacebo branch (k_tile<..., LP = 1>): 255 (x ainv)^(1/2.4) - 255 b =
+  // exp2(log2(x)/2.4 + lp_k1) - lp_k2, x clamped to [0, lp_xmax] (v >= 1 above);
+  // lut3d's 8-bit coordinate (q * inv255) * nm1; BT.709 rows at depth q
+  float lp_k1, lp_k2, lp_xmax, nm1, inv255, qscale, c56;
+  float k709[3], kcb[3], kcr[3];
   const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
@@ -136,6 +145,7 @@ constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
 
 struct YuvLutConsts {
   float s, k709[3], kcb[3], kcr[3];
+  int rgb;  // 1: plain R'G'B' records (the libplacebo branch truncates lut3d's output before Y'CbCr)
 };
 
 // ---- fast transcendentals (v_log_f32 / v_exp_f32 / v_rcp_f32) ----------

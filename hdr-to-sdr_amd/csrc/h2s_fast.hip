@@ -1,566 +1,17 @@
-// h2s_fast.hip — specialised fast path of the fused tone-map kernel.
-//
-// Same chain as k_generic (h2s_kernels.hip) and oracle/h2s_oracle.c, restated
-// for throughput on gfx950:
-//  * one template instance per (transfer, operator, desat): the 8 steps a wave
-//    runs per tile are straight-line code the compiler can interleave;
-//  * chroma upsampling on integer-valued floats (exact), the 1/4, 1/8 and
-//    depth-normalisation scales folded into the Y'CbCr->R'G'B' constants;
-//  * the 3D-LUT lattice pre-multiplied into output Y'CbCr code space
-//    (RGB->Y'CbCr is linear and the lattice lies in [0,1], so the swscale
-//    clip is a no-op and blend-then-convert == convert-then-blend); the
-//    tetrahedral blend then yields quantiser inputs directly;
-//  * lattice gathers are buffer loads (32-bit offsets, one SGPR base);
-//  * eq's table sits in LDS.
-// Geometry (k_tile): a block of 256 threads walks 8 consecutive 64 x 32 luma
-// tiles, prefetching tile i+1 into registers while tile i computes.  A tile
-// (Y, and U/V with their 1-row halo) is staged into LDS with coalesced
-// 16-byte loads; then, in 8 steps, each wave processes one dense 8 x 8 pixel
-// sub-block with one pixel per lane (lanes 4q..4q+3 = one 2x2 quad).  Dense
-// sub-blocks keep the 64 lanes of every lattice gather on few cache lines;
-// chroma is reduced per quad with DPP quad permutes and all outputs leave
-// through LDS as 16-byte coalesced stores.  Measured balance (DESIGN.md
-// §4.1): VALU ~70 % busy, LDS ~47 %, vector-memory return ~35 %.
+// h2s_fast.hip — launcher of the tile kernel (h2s_tile.h): the product
+// instances, the dispatch over every instance, and the Y'CbCr lattice build.
 #include <hip/hip_runtime.h>
 
-#include "h2s_device.h"
+#include "h2s_tile.h"
 
 namespace h2s {
 
-typedef float f3 __attribute__((ext_vector_type(3)));
-typedef unsigned u2v __attribute__((ext_vector_type(2)));
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
-
-// streaming frame I/O: non-temporal so the pixels do not evict LUT lines
-__device__ __forceinline__ uint2 nt_ld2(const uint8_t* p) {
-  const u2v v = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p));
-  return make_uint2(v.x, v.y);
-}
-__device__ __forceinline__ uint4 nt_ld4(const uint8_t* p) {
-  const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void nt_st2(uint2 w, uint8_t* p) {
-  __builtin_nontemporal_store(u2v{w.x, w.y}, reinterpret_cast<u2v*>(p));
-}
-__device__ __forceinline__ void nt_st4(uint4 w, uint8_t* p) {
-  __builtin_nontemporal_store(u4v{w.x, w.y, w.z, w.w}, reinterpret_cast<u4v*>(p));
-}
-
-__device__ __forceinline__ int fedge(int i, int n) {
-  i = i < 0 ? -i : i;
-  return i > n - 1 ? n - 1 : i;
-}
-
-__device__ __forceinline__ long long fxcd_remap(long long b, long long nb) {
-  const long long xcd = b & 7, idx = b >> 3, per = nb >> 3, rem = nb & 7;
-  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
-}
-
-// exact zimg st_2084_eotf x 10000/npl (used above the table's range)
-__device__ __forceinline__ float pq_exact(const FastParams& F, float e) {
-  const float xp = fexp2(flog2(fmaxf(e, 0.0f)) * (1.0f / PQ_M2));
-  const float num = fmaxf(xp - PQ_C1, 0.0f);
-  const float den = fmaxf(PQ_C2 - PQ_C3 * xp, 1.17549435e-38f);  // zimg: max(.., FLT_MIN)
-  return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + F.log2_lin_scale);
-}
-
-// Zero-segment form used by k_tile: the LDS table holds a zero segment at
-// index 0 and segment i of pq_tab at i+1, and the caller passes
-// u = E*PQ_SEG + 1 (the +1 is folded into the staged luma).  v_cvt_u32_f32
-// saturates negatives to 0, so E < 0 reads the zero segment (EOTF = 0) with no
-// clamp; at and past PQZ_LIM the value is garbage and the caller takes the
-// exact path.  The byte offset is formed with a 16-bit shift (full rate; bits
-// 31:16 are written as zero on gfx950, and the index fits 12 bits).
-__device__ __forceinline__ float pq_z(const float4* tab, float u) {
-  unsigned off;
-  asm("v_cvt_u32_f32 %0, %1\n\tv_lshlrev_b16 %0, 4, %0" : "=v"(off) : "v"(u));
-  const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + off);
-  const float t = __builtin_amdgcn_fractf(u);
-  return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
-}
-// staged E (table-segment units, +1) at and above which pq_z is invalid
-constexpr float PQZ_LIM = PQ_EMAX * (float)PQ_SEG + 1.0f;
-
-// S1 transfer to linear (units of npl), specialised
-// returns true (wave-uniform) when some lane of the wave took the exact PQ
-// path: linear values may then be huge or infinite, and the tone curve must
-// use its overflow-safe form
-template <int TRC, int ESC = 1>
-__device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
-                                          float& r, float& g, float& b) {
-  if (TRC == 0) {
-    // E arrives as E*PQ_SEG + 1 (pq_z)
-    static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
-    r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
-    const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
-    constexpr float EI = 1.0f / (float)PQ_SEG;
-    if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {  // rare: extreme out-of-gamut codes
-      r = er >= PQZ_LIM ? pq_exact(F, (er - 1.0f) * EI) : r;
-      g = eg >= PQZ_LIM ? pq_exact(F, (eg - 1.0f) * EI) : g;
-      b = eb >= PQZ_LIM ? pq_exact(F, (eb - 1.0f) * EI) : b;
-      return true;
-    }
-    return false;
-  } else {
-    // zimg arib_b67_inverse_oetf, branch-free; then the OOTF (gamma 1.2)
-    auto inv = [](float e) -> float {
-      const float x = fmaxf(e, 0.0f);
-      const float lo = (x * x) * (1.0f / 3.0f);
-      const float hi = (fexp2((x - HLG_C) * (1.4426950408889634f / HLG_A)) + HLG_B) * (1.0f / 12.0f);
-      return x <= 0.5f ? lo : hi;
-    };
-    r = inv(er), g = inv(eg), b = inv(eb);
-    const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
-    const float w = fexp2(flog2(ys) * 0.2f + F.log2_lin_scale);  // ys == 0 -> 0
-    r *= w, g *= w, b *= w;
-    return false;  // HLG is bounded (E <= 2.2 -> a few 1e4)
-  }
-}
-
-// S2 vf_tonemap, specialised.  DESAT: 0 off, 1 weighted luma (F.lr/lg/lb),
-// 2 the RGB-coefficient luma r+g+b (vf_tonemap's table entry for the linear
-// RGB frame zscale hands it; the default).
-//
-// Bounded form (every lane's linear values from the PQ table or HLG, so
-// sig <= ~6e8 and den*sig cannot overflow): the desaturation and the gain
-// fold into out = c*A + B with A = (1-ob)*k, B = L*ob*k, since
-// max(c*(1-ob) + L*ob) = max(c)*(1-ob) + L*ob for 0 <= ob <= 1; the curve
-// uses one reciprocal.  Safe form (the wave met the exact PQ path): the
-// statement order of vf_tonemap, two reciprocals.
-//
-// BT.2390 on PQ input (TRC 0, bounded form): the EETF's first step encodes
-// sig = max(R,G,B) back to PQ, and PQ(EOTF(max E)) = max E, so e1 is the
-// input's own max code value (emax_s = max E * PQ_SEG + 1, clamped below at
-// the code of sig = 1e-6); the final decode reads the EOTF table in LDS.
-template <int TRC, int TM, int DESAT>
-__device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds, float& r,
-                                     float& g, float& b, bool safe, float emax_s) {
-  if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
-    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-    float e1;
-    if (TRC == 0 && !safe) {
-      e1 = fmaxf(fmaf(emax_s, 1.0f / (float)PQ_SEG, -1.0f / (float)PQ_SEG), F.b_e1min);
-    } else {  // exact PQ encode: HLG input, or the wave met the exact EOTF path
-      const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
-      e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
-    }
-    float s2;
-    if (TRC == 0) {
-      // the curve straight into pq_z's table coordinate u = e4*PQ_SEG + 1:
-      // the output scale and offset are folded into the polynomial
-      // coefficients on the host (resolve_fast)
-      float u;
-      if (TM == 7) {   // BT.2390 Hermite knee as one cubic in t, Horner form
-        const float e1n = __builtin_amdgcn_fmed3f(fmaf(e1, C.b_e1a, C.b_e1b), 0.0f, 1.0f);
-        const float t = fmaf(e1n, C.b_ta, C.b_tb);
-        const float uk = fmaf(fmaf(fmaf(C.b_c3, t, C.b_c2), t, C.b_c1), t, C.b_c0);
-        u = e1n > C.b_thr ? uk : fmaf(e1n, C.b_lr, C.b_lc);
-      } else {         // spline: cubic shoulder / quadratic toe around the knee
-        const float x = __builtin_amdgcn_fmed3f(e1, C.sp_srcmin, C.sp_srcmax) - C.sp_kin;
-        const float uq = fmaf(fmaf(fmaf(C.sp_qa_u, x, C.sp_qb_u), x, C.sp_qc_u), x, C.sp_k_u);
-        const float up = fmaf(fmaf(C.sp_pa_u, x, C.sp_pb_u), x, C.sp_k_u);
-        u = __builtin_amdgcn_fmed3f(x > 0.0f ? uq : up, C.sp_umin, C.sp_umax);
-      }
-      s2 = pq_z(pq_lds, u);                                       // EOTF(e4) * 10000/npl
-    } else {
-      float e4;
-      if (TM == 7) {
-        const float e1n = fmaxf(fminf((e1 - C.b_srcmin) * C.b_inv_range, 1.0f), 0.0f);
-        const float t = (e1n - C.b_ks) * C.b_inv_1mks;
-        const float t2 = t * t, t3 = t2 * t;
-        const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * C.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - C.b_ks) +
-                        (-2.0f * t3 + 3.0f * t2) * C.b_maxlum;
-        const float e2 = (C.b_ks < 1.0f && e1n > C.b_ks) ? p : e1n;
-        e4 = fmaxf(e2 * C.b_range + C.b_srcmin, 0.0f);   // <= source max <= 1
-      } else {
-        e4 = spline_pq(C, e1);                            // within [PQ(0), PQ(npl)]
-      }
-      const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
-      s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
-    }
-    const float k = s2 * frcp(sig);
-    r *= k, g *= k, b *= k;
-    return;
-  }
-  if (safe) {
-    if (DESAT) {
-      const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
-      const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
-      const float iob = 1.0f - ob;
-      r = r * iob + luma * ob;
-      g = g * iob + luma * ob;
-      b = b * iob + luma * ob;
-    }
-    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-    float k;
-    if (TM == 4) {  // REINHARD: sig/(sig+p) * (peak+p)/peak
-      k = F.rein_k * frcp(sig + F.rein_p);
-    } else if (TM == 5) {  // HABLE: hable(sig) / hable(peak)
-      const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
-      const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
-      k = fmaf(num * frcp(den), F.hable_peak_inv, -F.hable_ef_peak_inv) * frcp(sig);
-    } else {  // MOBIUS: identity below j
-      const float m = F.mob_k * (sig + F.mob_a) * frcp(sig + F.mob_b) * frcp(sig);
-      k = sig <= F.mob_j ? 1.0f : m;
-    }
-    r *= k, g *= k, b *= k;
-    return;
-  }
-  float sig, A = 1.0f, B = 0.0f;
-  if (DESAT) {
-    const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
-    const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
-    A = 1.0f - ob, B = luma * ob;
-    sig = fmaxf(fmaf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), A, B), 1e-6f);
-  } else {
-    sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-  }
-  float k;
-  if (TM == 4) {
-    k = F.rein_k * frcp(sig + F.rein_p);
-  } else if (TM == 5) {
-    // hable(x) = N/D - e/f with 15 N - D = x (2.1 x + 0.25) (the constant
-    // terms cancel: d*e*15 = d*f), so hable(x)/x = (0.14 x + 1/60) / D:
-    // one reciprocal, no cancellation, and sig drops out of the gain
-    const float den = fmaf(sig, fmaf(sig, 0.15f, 0.50f), 0.06f);
-    k = fmaf(sig, F.hable_ka, F.hable_kb) * frcp(den);
-  } else {
-    const float m = F.mob_k * (sig + F.mob_a) * frcp((sig + F.mob_b) * sig);
-    k = sig <= F.mob_j ? 1.0f : m;
-  }
-  if (DESAT) {
-    A *= k, B *= k;
-    r = fmaf(r, A, B), g = fmaf(g, A, B), b = fmaf(b, A, B);
-  } else {
-    r *= k, g *= k, b *= k;
-  }
-}
-
-// S3 + S4 coordinates: s = clamp((N-1) * x^(1/2.4)), as lattice units
-// NaN -> 0 (lut3d sanitizef), +inf -> top of the lattice
-__device__ __forceinline__ float lut_s(const FastParams& F, float x) {
-  return fminf(fmaxf(fexp2(flog2(x) * (1.0f / 2.4f) + F.log2_nm1), 0.0f), F.s_max);
-}
-
-
-constexpr int TBW = 64, TBH = 32;  // luma tile of one block
-constexpr int CBW = 32, CBH = 16;  // chroma tile
-constexpr int YST = 68;            // LDS row stride (floats) of the luma tile
-constexpr int HST = 68;            // LDS row stride of the horizontally upsampled chroma rows
-constexpr int NT = 2;              // buffer-op aux bits: non-temporal (streamed frame bytes)
-
-__device__ __forceinline__ float quad_sum(float v) {
-  // (v0 + v1) + (v2 + v3) over the 2x2 pixels of a quad, in all 4 lanes
-  // (quad_perm [1,0,3,2] pairs horizontally, then [2,3,0,1] adds the rows):
-  // the oracle's summation order, so the chroma sum is bit-identical
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ void unpack8(const uint4 a, float* o) {
-  o[0] = (float)(a.x & 0xffff), o[1] = (float)(a.x >> 16), o[2] = (float)(a.y & 0xffff), o[3] = (float)(a.y >> 16);
-  o[4] = (float)(a.z & 0xffff), o[5] = (float)(a.z >> 16), o[6] = (float)(a.w & 0xffff), o[7] = (float)(a.w >> 16);
-}
-
-// keep a wave-uniform constant in a VGPR (avoids per-use SGPR->VGPR moves
-// forced by the one-scalar-operand limit of VOP3 on gfx950)
-template <class T>
-__device__ __forceinline__ T in_vgpr(T x) {
-  T y;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
-  return y;
-}
-
-// bytes: the plane's extent, clamped to 2^31-1 on the host (FastParams in/out_bytes)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
-}
-
-// one tile's global loads, held in registers between issue and the LDS commit
-struct TileRegs {
-  uint4 ya, ua, va;
-  unsigned uh, vh;
-};
-
-struct TileGeo {
-  int f, px0, py0, cx0, cy0;
-};
-
-// frame f's curve record: a constant-address-space load with a block-uniform
-// index, so the compiler emits scalar (s_load) reads
-__device__ __forceinline__ CurveConsts curve_of(const CurveConsts* frames, int f) {
-  typedef __attribute__((address_space(4))) const float cfloat;
-  constexpr int n = (int)(sizeof(CurveConsts) / sizeof(float));
-  cfloat* src = (cfloat*)frames + __builtin_amdgcn_readfirstlane(f) * n;
-  CurveConsts r;
-  float* dst = reinterpret_cast<float*>(&r);
-#pragma unroll
-  for (int i = 0; i < n; i++) dst[i] = src[i];
-  return r;
-}
-
-__device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) {
-  const unsigned bx = tile % F.nbx, bt = tile / F.nbx;
-  TileGeo g;
-  g.f = (int)(bt / F.nby);
-  const int by = (int)(bt % F.nby);
-  g.px0 = (int)bx * TBW, g.py0 = by * TBH, g.cx0 = (int)bx * CBW, g.cy0 = by * CBH;
-  return g;
-}
-
-// the tile after g in walk order (x, then y, then frame): block-uniform
-// scalar arithmetic, no division
-__device__ __forceinline__ void tile_next(const FastParams& F, TileGeo& g) {
-  g.px0 += TBW, g.cx0 += CBW;
-  if (g.px0 >= F.W) {
-    g.px0 = 0, g.cx0 = 0, g.py0 += TBH, g.cy0 += CBH;
-    if (g.py0 >= (int)F.nby * TBH) g.py0 = 0, g.cy0 = 0, g.f++;
-  }
-}
-
-// issue (do not wait for) the loads of one tile: luma 64 x 32 (one 16-byte
-// load per thread) and chroma rows cy0-1 .. cy0+16 (18 rows x 4 chunks of 8
-// samples + 1 right-halo sample; threads 0..71).  One thread loads the same
-// chunk of both planes, so each buffer resource stays wave-uniform (a per-lane
-// choice of resource becomes a waterfall loop).
-__device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t) {
-  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], F.in_bytes[0]);
-  const int yr = t >> 3, yc = t & 7;
-  TileRegs r;
-  r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                       iy, (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), 0, NT));
-  r.ua = r.va = make_uint4(0, 0, 0, 0);
-  r.uh = r.vh = 0;
-  if (t < 72) {
-    const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], F.in_bytes[1]);
-    const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], F.in_bytes[2]);
-    const int clr = t >> 2, ccx = t & 3;
-    const int row = fedge(g.cy0 - 1 + clr, F.ch), hx = 2 * fedge(g.cx0 + 8 * ccx + 8, F.cw);
-    const int ou = row * (int)F.in_ls[1], ov = row * (int)F.in_ls[2];
-    r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iu, ou + 2 * (g.cx0 + 8 * ccx), 0, NT));
-    r.va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iv, ov + 2 * (g.cx0 + 8 * ccx), 0, NT));
-    r.uh = __builtin_amdgcn_raw_buffer_load_b16(iu, ou + hx, 0, 0);
-    r.vh = __builtin_amdgcn_raw_buffer_load_b16(iv, ov + hx, 0, 0);
-  }
-  return r;
-}
-
-// Each block walks F.tpb consecutive tiles (XCD-remapped, so neighbouring
-// tiles and their lattice cells share one XCD's L2).  The loads of tile i+1
-// are issued before tile i is computed, so after the first tile the block no
-// longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
-// barrier, 8 compute steps, barrier, store, barrier.
-// DBG (debug instances only, never launched by h2s_process): 1..5 = also
-// write that h2s_stage's three float planes for frame 0 to F.dbg (W x H each)
-// from this kernel's own arithmetic — stage 4 blends the float4 RGB lattice
-// F.dbg_lut with the same cell, corners and weights as the Y'CbCr lattice
-template <int TRC, int TM, int DESAT, int DBG = 0>
-// 5 waves per SIMD = the LDS-bound occupancy (5 blocks of ~27.6 KB per CU;
-// 3 and 6 measured slower): let the compiler use the VGPRs that allows
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
-  __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
-  __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
-  __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
-  __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
-  extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
-  // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
-  // folded into the Y'CbCr->R'G'B' constants)
-  constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
-
-  const int t = threadIdx.x;
-  const unsigned ntiles = F.nbx * F.nby * F.nframes;
-  unsigned tile = (unsigned)fxcd_remap(blockIdx.x, gridDim.x) * (unsigned)F.tpb;
-  const unsigned tend = tile + (unsigned)F.tpb < ntiles ? tile + (unsigned)F.tpb : ntiles;
-
-  // ---- prologue: first tile + tables, all issued before any wait ----
-  TileGeo geo = tile_geo(F, tile);
-  TileRegs cur = tile_load(F, geo, t);
-  const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
-  const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * t, 0, 0);  // out of range -> 0
-  float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (TRC == 0 && t < PQ_NSEG) {
-    const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
-    pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
-  }
-  if (t < F.eq_n) eq_lds[t] = (uint16_t)(eq0 << F.shift_out);
-  for (int i = t + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
-    eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
-  if (TRC == 0 && t < PQ_NSEG) pq_lds[t + 1] = pq0;
-  if (TRC == 0 && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-
-  // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block
-  // (2w + (s&1), s>>1); lane = pixel (quad q = lane>>2 in a 4x4 quad grid,
-  // position lane&3 in the quad) ----
-  const int lane = t & 63, w = t >> 6;
-  const int qx = (lane >> 2) & 3, qy = lane >> 4, pxl = lane & 1, pyl = (lane >> 1) & 1;
-  const int xl = 16 * w + 2 * qx + pxl, yl = 2 * qy + pyl;                 // step (0,0) pixel
-  const float* ybase = yin + yl * YST + xl;
-  // vertical pass (centre siting): 3 x row cy + row cy-1 (top) / cy+1 (bottom)
-  const float* h0 = hrow[0] + (qy + 1) * HST + xl;
-  const float* h1 = hrow[1] + (qy + 1) * HST + xl;
-  const int hb = pyl ? HST : -HST;
-  float* csb = csum[0] + qy * CBW + 8 * w + qx;
-
-  // hot constants live in VGPRs for the whole kernel.  Staged samples:
-  // luma Y*ys + y_off (+1 on PQ: pq_z's zero segment), chroma centred on its
-  // midpoint code (exact), so E = Y' + a*{U,V} takes 4 FMAs
-  const float yoff = in_vgpr(F.y_off_c) * (float)ESC + (TRC == 0 ? 1.0f : 0.0f);
-  const float cmid = in_vgpr(F.c_mid);
-  const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
-              a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
-  const float stride_g = in_vgpr(F.stride_g), stride_b = in_vgpr(F.stride_b);
-  const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
-  const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
-  const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
-
-  for (;;) {
-    // ---- commit this tile's registers to LDS ----
-    {
-      float v[8];
-      unpack8(cur.ya, v);
-      float* d = yin + (t >> 3) * YST + 8 * (t & 7);
-      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
-      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
-    }
-    if (t < 72) {
-      // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
-      // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float
-      auto put = [&](const uint4 a, unsigned h, float* plane) {
-        float v[9];
-        unpack8(a, v);
-        v[8] = (float)h;
-#pragma unroll
-        for (int k = 0; k < 9; k++) v[k] -= cmid;
-        float* d = plane + (t >> 2) * HST + 16 * (t & 3);
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          *reinterpret_cast<float4*>(d + 4 * k) =
-              make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
-      };
-      put(cur.ua, cur.uh, hrow[0]);
-      put(cur.va, cur.vh, hrow[1]);
-    }
-    const TileGeo g = geo;
-    // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
-    // frame, read through the scalar cache; the frame index is block-uniform)
-    CurveConsts cv = F;
-    if ((TM == 7 || TM == 8) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
-    const bool more = tile + 1 < tend;   // block-uniform
-    if (more) {
-      tile_next(F, geo);
-      cur = tile_load(F, geo, t);        // in flight during this tile's compute
-    }
-    __syncthreads();
-
-    const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
-      const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
-      const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
-      const float ybs = ybase[oy];
-      const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
-      const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
-      const float er = fmaf(V, a_rv, ybs);
-      const float eg = fmaf(V, a_gv, fmaf(U, a_gu, ybs));
-      const float eb = fmaf(U, a_bu, ybs);
-      float r, gg, bl;
-      const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
-      // debug: this step's pixel in frame 0 (plane index), -1 = not written
-      const long long di = DBG && g.f == 0 && g.py0 + yl + 8 * (s >> 1) < F.H
-                               ? (long long)(g.py0 + yl + 8 * (s >> 1)) * F.dbg_w + g.px0 + xl + 8 * (s & 1)
-                               : -1;
-      const long long dpl = (long long)F.dbg_w * F.H;
-      auto dput = [&](float a, float b_, float c) {
-        if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
-      };
-      if (DBG == 1) dput(r, gg, bl);
-      tone<TRC, TM, DESAT>(F, cv, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
-      if (DBG == 2) dput(r, gg, bl);
-      // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
-      // s < N-1 and the lattice cell index never needs a clamp
-      const float sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-      const float sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-      const float sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-      const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-      const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
-      const bool rg = dr > dg, gb = dg > db, rb = dr > db;
-      const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
-      const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
-      const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
-      const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
-      const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
-      const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0);
-      const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0);
-      const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0);
-      const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
-      const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
-      const f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
-      if (DBG == 3) dput(sr * F.inv_nm1, sg * F.inv_nm1, sb * F.inv_nm1);
-      if (DBG == 4) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
-        const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
-                     q3 = F.dbg_lut[(base + F.c111) / 12];
-        dput(w0 * q0.x + w1 * q1.x + w2 * q2.x + w3 * q3.x, w0 * q0.y + w1 * q1.y + w2 * q2.y + w3 * q3.y,
-             w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
-      }
-      if (DBG == 5) dput(o.x - 0.5f, 4.0f * o.y, 4.0f * o.z);
-      // luma code (eq applied, shifted) replaces the luma sample this lane read
-      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = eq_lds[(int)o.x];
-      // chroma: 2x2 sums; the 4 lanes of a quad store the same value
-      const float su = quad_sum(o.y), sv = quad_sum(o.z);
-      csb[oc] = su;
-      csb[oc + CBH * CBW] = sv;
-    }
-    __syncthreads();
-
-    // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
-    {
-      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
-      const int r = t >> 3, c = t & 7;
-      if (g.py0 + r < F.H) {
-        const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
-        const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
-        const int off = (g.py0 + r) * (int)F.out_ls[0];
-        if (F.out8)
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
-              oy_, off + g.px0 + 8 * c, 0, NT);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
-              oy_, off + 2 * (g.px0 + 8 * c), 0, NT);
-      }
-    }
-    if (t < 128) {
-      // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
-      const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
-      if (g.cy0 + r < F.ch) {
-        const float4* src = reinterpret_cast<const float4*>(csum[pl] + r * CBW + 8 * c);
-        const float4 v0 = src[0], v1 = src[1];
-        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        unsigned code[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
-        const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
-        const int off = (g.cy0 + r) * (int)F.out_ls[1 + pl];
-        if (F.out8)
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
-                                                 code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
-              oc_, off + g.cx0 + 8 * c, 0, NT);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
-                                                 code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
-              oc_, off + 2 * (g.cx0 + 8 * c), 0, NT);
-      }
-    }
-    if (!more) break;
-    ++tile;
-    __syncthreads();   // the store phase has read yin / csum before they are refilled
-  }
-}
+H2S_TILE_INSTANCE(0)
+H2S_TILE_EXTERN(1)
+H2S_TILE_EXTERN(2)
+H2S_TILE_EXTERN(3)
+H2S_TILE_EXTERN(4)
+H2S_TILE_EXTERN(5)
 
 // YUV-premultiplied lattice (12-byte records, .cube order):
 // ((16 + 219*Y)*s + 0.5, 224*s*Cb/4, 224*s*Cr/4) with Y, Cb, Cr the BT.709
@@ -574,61 +25,36 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
   const float cb = K.kcb[0] * R + K.kcb[1] * G + K.kcb[2] * B;
   const float cr = K.kcr[0] * R + K.kcr[1] * G + K.kcr[2] * B;
   const float s = K.s;
+  if (K.rgb) {  // plain R'G'B' (libplacebo branch): lut3d's own lattice values, unclamped
+    yuv[3 * i] = c.x, yuv[3 * i + 1] = c.y, yuv[3 * i + 2] = c.z;
+    return;
+  }
   yuv[3 * i] = (16.0f + 219.0f * Y) * s + 0.5f;
   yuv[3 * i + 1] = 224.0f * s * 0.25f * cb;
   yuv[3 * i + 2] = 224.0f * s * 0.25f * cr;
 }
 
-#define FAST_CASES(X) \
-  X(0, 4, 0)          \
-  X(0, 4, 1)          \
-  X(0, 4, 2)          \
-  X(0, 5, 0)          \
-  X(0, 5, 1)          \
-  X(0, 5, 2)          \
-  X(0, 6, 0)          \
-  X(0, 6, 1)          \
-  X(0, 6, 2)          \
-  X(0, 7, 0)          \
-  X(0, 8, 0)          \
-  X(1, 4, 0)          \
-  X(1, 4, 1)          \
-  X(1, 4, 2)          \
-  X(1, 5, 0)          \
-  X(1, 5, 1)          \
-  X(1, 5, 2)          \
-  X(1, 6, 0)          \
-  X(1, 6, 1)          \
-  X(1, 6, 2)          \
-  X(1, 7, 0)          \
-  X(1, 8, 0)
-
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
-// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma.  dbg: 0 = the
+// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma.  lp: the
+// libplacebo branch's rgba8 form (BT.2390 / spline only).  dbg: 0 = the
 // product kernel; 1..5 = its debug instance for that h2s_stage (F.dbg set)
-hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, hipStream_t s, int dbg) {
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
   if (nt == 0) return hipSuccess;
   const long long nb = (nt + F.tpb - 1) / F.tpb;
-  dim3 grid((unsigned)nb), block(256);
+  dim3 grid((unsigned)nb);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8) desat = 0;
-#define X(T, M, D)                                                                        \
-  if (trc == T && tm == M && desat == D) {                                                \
-    switch (dbg) {                                                                        \
-      case 0: hipLaunchKernelGGL((k_tile<T, M, D, 0>), grid, block, lds, s, F); break;    \
-      case 1: hipLaunchKernelGGL((k_tile<T, M, D, 1>), grid, block, lds, s, F); break;    \
-      case 2: hipLaunchKernelGGL((k_tile<T, M, D, 2>), grid, block, lds, s, F); break;    \
-      case 3: hipLaunchKernelGGL((k_tile<T, M, D, 3>), grid, block, lds, s, F); break;    \
-      case 4: hipLaunchKernelGGL((k_tile<T, M, D, 4>), grid, block, lds, s, F); break;    \
-      default: hipLaunchKernelGGL((k_tile<T, M, D, 5>), grid, block, lds, s, F); break;   \
-    }                                                                                     \
-    return hipGetLastError();                                                             \
+  else lp = 0;
+  switch (dbg) {
+    case 0: return launch_tile<0>(F, trc, tm, desat, lp, grid, lds, s);
+    case 1: return launch_tile<1>(F, trc, tm, desat, lp, grid, lds, s);
+    case 2: return launch_tile<2>(F, trc, tm, desat, lp, grid, lds, s);
+    case 3: return launch_tile<3>(F, trc, tm, desat, lp, grid, lds, s);
+    case 4: return launch_tile<4>(F, trc, tm, desat, lp, grid, lds, s);
+    default: return launch_tile<5>(F, trc, tm, desat, lp, grid, lds, s);
   }
-  FAST_CASES(X)
-#undef X
-  return hipErrorInvalidValue;
 }
 
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st) {

@@ -211,6 +211,10 @@ FLOAT_CFGS = {
     'C3_bt2390_pq10_cpu': dict(tonemapper='bt.2390', pipeline='cpu', bits_out=10),
     'C5_hable_hlg12': dict(tonemapper='hable', bits_in=12, bits_out=12, transfer='arib-std-b67'),
     'C4_mobius_native': dict(tonemapper='mobius', bits_out=10, mode='native'),
+    # the libplacebo branch (the reference's C3 chain, src/utils.py:444-460):
+    # knee offset 1.0, black point 0.203 nits, target white 203, rgba8 + lut3d 8-bit
+    'C3_bt2390_libplacebo': dict(tonemapper='bt.2390', bits_out=10),
+    'spline_libplacebo_hlg12': dict(tonemapper='spline', bits_in=12, bits_out=12, transfer='arib-std-b67'),
 }
 
 
@@ -264,10 +268,32 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
     assert skip.mean() < (0.1 if kind == 'edges' else 0.01)
     keep = np.broadcast_to(~skip[None], want.shape)
     assert np.isfinite(want[keep]).all() and np.isfinite(got[keep]).all()
+    if stage == 2:
+        # stage 2 scales each pixel by its tone gain k = s2 / max(R,G,B); the
+        # stage-1 floor propagates as floor * k.  k <= ~1 for the CPU chain,
+        # but libplacebo's black-point lift raises the darkest pixels to the
+        # target black (0.203 nits), k up to ~100
+        import warnings
+        with np.errstate(invalid='ignore', divide='ignore'), warnings.catch_warnings():
+            warnings.simplefilter('ignore', RuntimeWarning)     # all-NaN pixels ('edges' codes)
+            gain = np.nanmax(np.abs(want), axis=0) / np.nanmax(np.abs(lin), axis=0)
+        floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None]
     tol = 1e-3 * np.abs(want) + floor
+    if params.resolved_pipeline() == 'libplacebo' and stage >= 4:
+        # after the 8-bit rgba download the values are quantised: 1e-3 holds
+        # wherever both sides rounded the download alike; a float-rounding flip
+        # (a stage-3 value within ~1e-4 of a half step) moves the lattice
+        # coordinate by (N-1)/255 and the truncated 8-bit LUT output by up to
+        # k8 steps (assert_close_int's bound): < 1 % of pixels, within k8 steps
+        k8 = math.ceil(_lattice_max_step(65) * 64) + 1
+        lim = k8 / 255.0 if stage == 4 else 224 * (1 << (q - 8)) * k8 / 255.0 + 1.0
+        flip = ((err > tol) & keep).any(axis=0)
+        assert flip.mean() < 0.01, f'{flip.mean():.3%} of pixels off after the rgba8 download'
+        assert (err[keep] <= lim).all(), f'max {float(err[keep].max()):.4g} > {lim:.4g}'
+        return
     bad = (err > tol) & keep
     i = int(np.argmax(np.where(bad, err / tol, 0)))
-    assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {floor:g} '
+    assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {float(np.max(floor)):g} '
                            f'({int(skip.sum())} ill-conditioned pixels excluded); worst: want '
                            f'{float(want.flat[i]):.6g} got {float(got.flat[i]):.6g}')
 

@@ -107,6 +107,27 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
     assert params.resolved_pipeline() == 'libplacebo'
     got, want, wh = run_both(tm, params, kind, 128, 64)
     assert_close_int(params, got, want, *wh)
+    # with the LUT on, the branch runs on the tile kernel (k_tile<..., LP = 1>)
+    assert _path(tm, params, 128, 64) == (_abi.PATH_TILE if params.lut_enabled else _abi.PATH_GENERIC)
+
+
+@pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12'])
+def test_libplacebo_tile_equals_generic(tm, case):
+    """The two kernels of the libplacebo branch against each other (same
+    device, same float32 formulas up to the tile kernel's PQ table): the
+    bound of assert_close_int with the generic kernel as the reference."""
+    params = hdr2sdr.TonemapParams(**LP_CASES[case])
+    src = synth_frames('smooth', 2, 256, 64, params.bits_in, device='cpu', seed=4).to_torch('cuda')
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    tile = tm(src).to_numpy().buf.astype(np.int64)
+    tm.set_option(_abi.OPT_FAST_PATH, 0)
+    try:
+        gen = tm(src).to_numpy().buf.astype(np.int64)
+    finally:
+        tm.set_option(_abi.OPT_FAST_PATH, 1)
+    assert_close_int(params, tile, gen, 256, 64)
+    assert (tile == gen).mean() > 0.99
 
 
 def test_libplacebo_rgba_codes_use_the_full_output_depth(tm):
