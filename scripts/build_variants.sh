@@ -1,19 +1,28 @@
 #!/bin/bash
 # Build libh2s variants for scripts/time_variants.py.
 # Usage: bash scripts/build_variants.sh NAME:"-DFLAG ..." NAME2:"..."
+# Only the product tile instances (h2s_fast.hip) are rebuilt with the flags;
+# every other object comes from the in-tree build (hdr-to-sdr_amd/build/obj,
+# run `python -c "import __graft_entry__ as g; g.build()"` first).
 # Outputs scripts/variants/libh2s_NAME.so (git-ignored, travels with gpurun).
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/hdr-to-sdr_amd/csrc
-mkdir -p "$ROOT/scripts/variants"
+O=$ROOT/hdr-to-sdr_amd/build/obj
+V=$ROOT/scripts/variants
+mkdir -p "$V"
+FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed"
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   [ "$flags" = "$spec" ] && flags=""
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -shared -fPIC \
-    -Wno-unused-value -Wno-unused-result $flags -o "$ROOT/scripts/variants/libh2s_$name.so" \
-    "$C/h2s_api.hip" "$C/h2s_kernels.hip" "$C/h2s_fast.hip" "$C/h2s_preview.hip" "$C/h2s_cube.cpp" &
+  (
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fast_$name.o" "$C/h2s_fast.hip" &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" \
+      "$O/h2s_fast_dbg345.hip.o" "$O/h2s_fast_dbg12.hip.o" "$O/h2s_api.hip.o" "$O/h2s_kernels.hip.o" \
+      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o"
+  ) &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
-ls -la "$ROOT/scripts/variants"
+ls -la "$V"

@@ -54,8 +54,7 @@ UNARY_KERNEL(k_add, "v_add_f32 %0, %0, %0")
 UNARY_KERNEL(k_max, "v_max_f32 %0, %0, 1.0")
 UNARY_KERNEL(k_min, "v_min_f32 %0, %0, 1.0")
 UNARY_KERNEL(k_max3, "v_max3_f32 %0, %0, 1.0, %0")
-UNARY_KERNEL(k_cnd, "v_cndmask_b32 %0, %0, 1.0, vcc")
-UNARY_KERNEL(k_cnd64, "v_cndmask_b32_e64 %0, %0, 1.0, s[0:1]")
+
 UNARY_KERNEL(k_addu, "v_add_u32 %0, 7, %0")
 UNARY_KERNEL(k_lsh, "v_lshlrev_b32 %0, 1, %0")
 UNARY_KERNEL(k_and, "v_and_b32 %0, 7, %0")
@@ -64,7 +63,7 @@ UNARY_KERNEL(k_movdpp, "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf ba
 UNARY_KERNEL(k_adddpp, "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
 UNARY_KERNEL(k_floor, "v_floor_f32 %0, %0")
 UNARY_KERNEL(k_cvtf, "v_cvt_f32_i32 %0, %0")
-UNARY_KERNEL(k_cmp, "v_cmp_gt_f32 vcc, %0, 1.0")
+
 UNARY_KERNEL(k_fmaak, "v_fmaak_f32 %0, %0, %0, 0x3e000000")
 UNARY_KERNEL(k_mulu24, "v_mul_u32_u24 %0, 7, %0")
 UNARY_KERNEL(k_mullo, "v_mul_lo_u32 %0, %0, %0")
@@ -74,6 +73,65 @@ UNARY_KERNEL(k_cvtflr, "v_cvt_flr_i32_f32 %0, %0")
 UNARY_KERNEL(k_bfe, "v_bfe_u32 %0, %0, 4, 8")
 UNARY_KERNEL(k_andor, "v_and_or_b32 %0, %0, -16, 5")
 UNARY_KERNEL(k_lshl16, "v_lshlrev_b16 %0, 1, %0")
+
+// Instructions that read or write SGPR masks.  Every SGPR operand goes
+// through a constraint ("s" input / "=s" output) or a declared clobber
+// ("vcc"): an asm statement that names a fixed SGPR pair the compiler does
+// not know about can overwrite live state -- round 1's k_cmp64 wrote
+// s[0:1], the kernarg pointer on entry, and the final out[] store then
+// faulted (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION).
+#define CHAIN8_CNDVCC()                                                            \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x0) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x1) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x2) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x3) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x4) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x5) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x6) : : "vcc");           \
+  asm volatile("v_cndmask_b32 %0, %0, 1.0, vcc" : "+v"(x7) : : "vcc");
+#define CND64(X) asm volatile("v_cndmask_b32_e64 %0, %0, 1.0, %1" : "+v"(X) : "s"(m));
+#define CMP64(X) asm volatile("v_cmp_gt_f32_e64 %0, %1, 1.0" : "=s"(m) : "v"(X)); acc ^= m;
+#define CMPVCC(X) asm volatile("v_cmp_lt_f32_e32 vcc, 1.0, %0" : : "v"(X) : "vcc");
+
+__global__ __launch_bounds__(256) void k_cnd(float* out, float seed) {
+  float x0 = seed + threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5, x6 = x0 + 6,
+        x7 = x0 + 7;
+  for (int i = 0; i < ITERS; i++) {
+    CHAIN8_CNDVCC()
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7;
+}
+
+__global__ __launch_bounds__(256) void k_cnd64(float* out, float seed) {
+  float x0 = seed + threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5, x6 = x0 + 6,
+        x7 = x0 + 7;
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(x0 > 8.0f);  // an SGPR pair the compiler owns
+  for (int i = 0; i < ITERS; i++) {
+    CND64(x0) CND64(x1) CND64(x2) CND64(x3) CND64(x4) CND64(x5) CND64(x6) CND64(x7)
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7;
+}
+
+// compares: VOPC writing VCC (declared clobber) and VOP3 writing an SGPR pair
+// the compiler allocates ("=s"), folded into a scalar so none is dead
+__global__ __launch_bounds__(256) void k_cmp(float* out, float seed) {
+  const float x0 = seed + threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+              x6 = x0 + 6, x7 = x0 + 7;
+  for (int i = 0; i < ITERS; i++) {
+    CMPVCC(x0) CMPVCC(x1) CMPVCC(x2) CMPVCC(x3) CMPVCC(x4) CMPVCC(x5) CMPVCC(x6) CMPVCC(x7)
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = x0;
+}
+
+__global__ __launch_bounds__(256) void k_cmp64(float* out, float seed) {
+  const float x0 = seed + threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+              x6 = x0 + 6, x7 = x0 + 7;
+  unsigned long long m, acc = 0;
+  for (int i = 0; i < ITERS; i++) {
+    CMP64(x0) CMP64(x1) CMP64(x2) CMP64(x3) CMP64(x4) CMP64(x5) CMP64(x6) CMP64(x7)
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = x0 + (float)(acc & 1);
+}
 
 __global__ __launch_bounds__(256) void k_pkfma32(float* out, float seed) {
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -180,6 +238,7 @@ int main() {
       {"mix 1exp+3fma", k_mix13, 32},
       {"v_fmac_f32", k_fmac, 8}, {"v_add_f32", k_add, 8}, {"v_max_f32", k_max, 8}, {"v_min_f32", k_min, 8},
       {"v_max3_f32", k_max3, 8}, {"v_cndmask e32", k_cnd, 8}, {"v_cndmask e64", k_cnd64, 8},
+      {"v_cmp e32 (vcc)", k_cmp, 8}, {"v_cmp e64 (sgpr)", k_cmp64, 8},
       {"v_add_u32", k_addu, 8}, {"v_lshlrev_b32", k_lsh, 8}, {"v_and_b32", k_and, 8}, {"v_mov_b32", k_mov, 8},
       {"v_mov_b32_dpp", k_movdpp, 8}, {"v_add_f32_dpp", k_adddpp, 8}, {"v_floor_f32", k_floor, 8},
       {"v_mul_u32_u24", k_mulu24, 8}, {"v_mul_lo_u32", k_mullo, 8}, {"v_lshl_add_u32", k_lshladd, 8},
