@@ -139,6 +139,8 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_INVALID_ARG, "unknown dither");
   if (p->expand != H2S_EXPAND_SHIFT && p->expand != H2S_EXPAND_REPLICATE)
     return fail(c, H2S_E_INVALID_ARG, "unknown expand");
+  if (p->chroma_edge < H2S_EDGE_ZIMG || p->chroma_edge > H2S_EDGE_MIRROR)
+    return fail(c, H2S_E_INVALID_ARG, "unknown chroma_edge");
   if (p->pipeline < H2S_PIPE_AUTO || p->pipeline > H2S_PIPE_LIBPLACEBO)
     return fail(c, H2S_E_INVALID_ARG, "unknown pipeline");
   if (p->pipeline == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
@@ -329,6 +331,7 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   k->shift_out = p->bits_out - q;
   k->dither = p->dither == H2S_DITHER_ORDERED && q == 8 ? 1 : 0;
   k->expand_rep = p->expand == H2S_EXPAND_REPLICATE ? 1 : 0;
+  k->chroma_edge = p->chroma_edge;
   // S7 vf_eq create_lut, generalised to 2^q entries
   const int qn = 1 << q;
   eq->assign(qn, 0);
@@ -857,6 +860,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   // tile reads the real column (F.cw stays the frame's), so the split is exact
   const int w64 = k.W & ~63;
   F.W = w64, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
+  F.chroma_edge = k.chroma_edge;
   for (int p = 0; p < 3; p++) {
     const long long ib = (long long)(p ? k.ch : k.H) * k.in_ls[p], ob = (long long)(p ? k.ch : k.H) * k.out_ls[p];
     F.in_bytes[p] = (int)(ib < 0x7fffffff ? ib : 0x7fffffff);

@@ -58,6 +58,7 @@ struct KParams {
   float qscale;
   int eq_identity;
   const uint16_t* eq_lut;
+  int chroma_edge;        // S1 upsampler edge rule (chroma_edge_at)
   int dither;             // ordered 8x8 dither at the 8-bit quantiser
   int expand_rep;         // S8 bit replication instead of a shift
   // Y'CbCr 709 rows
@@ -67,6 +68,16 @@ struct KParams {
 };
 
 constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
+
+// S1 chroma upsampler edge rule (enum h2s_chroma_edge; oracle edge()): the
+// sample read at position i of an n-sample chroma row / column.  0 ZIMG: -1
+// mirrors to 1, n folds to n-1; 1 REPLICATE: both sides repeat the last
+// sample; 2 MIRROR: both sides mirror about it (n -> n-2)
+__host__ __device__ __forceinline__ int chroma_edge_at(int i, int n, int mode) {
+  if (i < 0) i = mode == 1 ? 0 : -i;
+  if (i > n - 1) i = mode == 2 ? 2 * (n - 1) - i : n - 1;
+  return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+}
 
 // Constants of the PQ-domain curves (BT.2390 / spline) in the fast kernel's
 // folded form.  They are the only parameters that change from frame to frame
@@ -89,6 +100,7 @@ struct CurveConsts {
 // with every scale folded into constants.
 struct FastParams : CurveConsts {
   int W, H, cw, ch;                // luma / chroma geometry (W % 64 == 0)
+  int chroma_edge;                 // S1 upsampler edge rule (chroma_edge_at)
   unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
   int tpb;                         // tiles walked by one block (k_tile prefetches tile i+1 during tile i)
   const uint8_t* in[3];

@@ -14,11 +14,8 @@
 
 namespace h2s {
 
-__device__ __forceinline__ int edge(int i, int n) {
-  // zimg bilinear edge rule (see oracle/h2s_oracle.c edge())
-  i = i < 0 ? -i : i;
-  return i > n - 1 ? n - 1 : i;
-}
+// the upsampler's edge rule (params.chroma_edge; oracle/h2s_oracle.c edge())
+__device__ __forceinline__ int edge(const KParams& P, int i, int n) { return chroma_edge_at(i, n, P.chroma_edge); }
 
 // XCD-aware block remap: hardware deals blocks round-robin over 8 XCDs;
 // give XCD x the contiguous logical range [x*per(+rem), ...).  Bijective.
@@ -48,7 +45,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
 
   // ---- chroma: rows cy-1, cy, cy+1; columns cx0 .. cx0+QPT (halo) ----
   float cu[3][QPT + 1], cv[3][QPT + 1];
-  const int crow[3] = {edge(cy - 1, ch), cy, edge(cy + 1, ch)};
+  const int crow[3] = {edge(P, cy - 1, ch), cy, edge(P, cy + 1, ch)};
   const bool full = cx0 + QPT <= cw;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -57,7 +54,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
     if (VEC && full && QPT == 4) {
       const uint2 a = *reinterpret_cast<const uint2*>(ru + 2 * cx0);
       const uint2 b = *reinterpret_cast<const uint2*>(rv + 2 * cx0);
-      const int hx = cx0 + 4 < cw ? cx0 + 4 : cw - 1;
+      const int hx = edge(P, cx0 + 4, cw);
       int su[5] = {(int)(a.x & 0xffff), (int)(a.x >> 16), (int)(a.y & 0xffff), (int)(a.y >> 16), ld16(ru, hx)};
       int sv[5] = {(int)(b.x & 0xffff), (int)(b.x >> 16), (int)(b.y & 0xffff), (int)(b.y >> 16), ld16(rv, hx)};
 #pragma unroll
@@ -68,7 +65,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
     } else {
 #pragma unroll
       for (int k = 0; k <= QPT; k++) {
-        const int x = cx0 + k < cw ? cx0 + k : cw - 1;
+        const int x = edge(P, cx0 + k, cw);
         cu[i][k] = (float)ld16(ru, x) * P.c_scale + P.c_off;
         cv[i][k] = (float)ld16(rv, x) * P.c_scale + P.c_off;
       }
@@ -212,11 +209,11 @@ __global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
   const int x = (int)(i % P.W), y = (int)(i / P.W);
   const int cw = P.cw, ch = P.ch;
   auto hpass = [&](int plane, int cyy) -> float {
-    const uint8_t* row = P.in[plane] + edge(cyy, ch) * P.in_ls[plane];
+    const uint8_t* row = P.in[plane] + edge(P, cyy, ch) * P.in_ls[plane];
     const int k = x >> 1;
-    const float a = (float)ld16(row, edge(k, cw)) * P.c_scale + P.c_off;
+    const float a = (float)ld16(row, edge(P, k, cw)) * P.c_scale + P.c_off;
     if (!(x & 1)) return a;
-    const float b = (float)ld16(row, edge(k + 1, cw)) * P.c_scale + P.c_off;
+    const float b = (float)ld16(row, edge(P, k + 1, cw)) * P.c_scale + P.c_off;
     return 0.5f * a + 0.5f * b;
   };
   auto up = [&](int plane) -> float {

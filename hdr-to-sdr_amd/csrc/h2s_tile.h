@@ -51,10 +51,6 @@ __device__ __forceinline__ void nt_st4(uint4 w, uint8_t* p) {
   __builtin_nontemporal_store(u4v{w.x, w.y, w.z, w.w}, reinterpret_cast<u4v*>(p));
 }
 
-__device__ __forceinline__ int fedge(int i, int n) {
-  i = i < 0 ? -i : i;
-  return i > n - 1 ? n - 1 : i;
-}
 
 __device__ __forceinline__ long long fxcd_remap(long long b, long long nb) {
   const long long xcd = b & 7, idx = b >> 3, per = nb >> 3, rem = nb & 7;
@@ -352,7 +348,8 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
     const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], F.in_bytes[1]);
     const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], F.in_bytes[2]);
     const int clr = t >> 2, ccx = t & 3;
-    const int row = fedge(g.cy0 - 1 + clr, F.ch), hx = 2 * fedge(g.cx0 + 8 * ccx + 8, F.cw);
+    const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
+    const int hx = 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
     const int ou = row * (int)F.in_ls[1], ov = row * (int)F.in_ls[2];
     r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iu, ou + 2 * (g.cx0 + 8 * ccx), 0, NT));
     r.va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iv, ov + 2 * (g.cx0 + 8 * ccx), 0, NT));

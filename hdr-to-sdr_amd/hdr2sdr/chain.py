@@ -57,6 +57,7 @@ _DITHER = {'none': _abi.DITHER_NONE, 'ordered': _abi.DITHER_ORDERED}
 _EXPAND = {'shift': _abi.EXPAND_SHIFT, 'replicate': _abi.EXPAND_REPLICATE}
 # which of the reference's two chains: 'auto' = libplacebo for the GPU-only
 # operators (the only chain that has them), the CPU chain otherwise
+_EDGE = {'zimg': _abi.EDGE_ZIMG, 'replicate': _abi.EDGE_REPLICATE, 'mirror': _abi.EDGE_MIRROR}
 _PIPELINE = {'auto': _abi.PIPE_AUTO, 'cpu': _abi.PIPE_CPU_CHAIN, 'libplacebo': _abi.PIPE_LIBPLACEBO}
 
 
@@ -94,6 +95,7 @@ class TonemapParams:
     knee_offset: float = math.nan   # BT.2390 knee offset (NaN: libplacebo's 1.0; 0.5 = ITU-R BT.2390)
     target_black: float = math.nan  # SDR target black, nits (NaN: pipeline default)
     target_white: float = math.nan  # SDR target white, nits (NaN: libplacebo 203, CPU chain npl)
+    chroma_edge: str = 'zimg'   # S1 upsampler edge rule ('zimg' | 'replicate' | 'mirror')
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
@@ -106,7 +108,7 @@ class TonemapParams:
         if self.desat_luma not in _DESAT_LUMA:
             raise ValueError(f'unknown desat_luma {self.desat_luma!r}')
         for name, table in (('chroma_filter', _CHROMA), ('dither', _DITHER), ('expand', _EXPAND),
-                            ('pipeline', _PIPELINE)):
+                            ('pipeline', _PIPELINE), ('chroma_edge', _EDGE)):
             if getattr(self, name) not in table:
                 raise ValueError(f'unknown {name} {getattr(self, name)!r}; expected one of {sorted(table)}')
         if self.pipeline == 'libplacebo' and tm not in GPU_ONLY_TONEMAPPERS:
@@ -169,6 +171,7 @@ class TonemapParams:
         p.knee_offset = self.knee_offset
         p.target_black = self.target_black
         p.target_white = self.target_white
+        p.chroma_edge = _EDGE[self.chroma_edge]
         return p
 
     def resolved_pipeline(self) -> str:

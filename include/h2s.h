@@ -116,6 +116,14 @@ enum h2s_chroma_filter { H2S_CHROMA_BOX = 0, H2S_CHROMA_BICUBIC = 1 };
  * dither offsets (ff_dither_8x8_128 / 128 of an LSB) instead of +0.5. */
 enum h2s_dither { H2S_DITHER_NONE = 0, H2S_DITHER_ORDERED = 1 };
 
+/* S1 chroma upsampler edge rule: the sample the
+ * bilinear 2-tap reads past the plane's edge (row -1 above the first chroma
+ * row, row ch below the last, column cw right of the last; left-sited chroma
+ * never reads column -1).  ZIMG: -1 mirrors to 1, ch / cw fold to the last
+ * sample (the round-1 model).  REPLICATE: every edge repeats its last
+ * sample.  MIRROR: every edge mirrors about its last sample (ch -> ch-2). */
+enum h2s_chroma_edge { H2S_EDGE_ZIMG = 0, H2S_EDGE_REPLICATE = 1, H2S_EDGE_MIRROR = 2 };
+
 /* S8 8-bit -> bits_out expansion after eq. */
 enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
 
@@ -185,7 +193,8 @@ typedef struct h2s_params {
   double target_white;   /* SDR target white (nits); NaN: LIBPLACEBO = 203
                           * (libplacebo's SDR white, BT.2408), CPU_CHAIN =
                           * npl                                            */
-  int32_t reserved[4];
+  int32_t chroma_edge;   /* enum h2s_chroma_edge (S1)                       */
+  int32_t reserved[3];
 } h2s_params;
 
 /* A batch of planar 4:2:0 frames (yuv420p / yuv420p10le / yuv420p12le).

@@ -48,7 +48,8 @@ class Params(ctypes.Structure):
         ('expand', ctypes.c_int32), ('pipeline', ctypes.c_int32),
         ('knee_offset', ctypes.c_double), ('target_black', ctypes.c_double),
         ('target_white', ctypes.c_double),
-        ('reserved', ctypes.c_int32 * 4),
+        ('chroma_edge', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 3),
     ]
 
 

@@ -641,17 +641,21 @@ static inline void wr(const h2s_frames *f, int plane, int frame, int x, int y, i
   }
 }
 
-/* zimg resize edge rule for the 2-tap bilinear kernel: position -1 mirrors
- * to 1, position n folds to n-1 (zimg resize/filter.cpp compute_filter). */
-static inline int edge(int i, int n) {
-  if (i < 0) i = -i;
-  if (i > n - 1) i = n - 1;
-  return i;
+/* S1 upsampler edge rule (h2s_params.chroma_edge; [EXT],
+ * not pinnable here).  ZIMG (default, the round-1 model of zimg
+ * resize/filter.cpp compute_filter for the 2-tap bilinear kernel): position
+ * -1 mirrors to 1, position n folds to n-1.  REPLICATE: both sides repeat
+ * the edge sample.  MIRROR: both sides mirror about it (n -> n-2). */
+static inline int edge_m(int i, int n, int mode) {
+  if (i < 0) i = mode == H2S_EDGE_REPLICATE ? 0 : -i;
+  if (i > n - 1) i = mode == H2S_EDGE_MIRROR ? 2 * (n - 1) - i : n - 1;
+  return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
 }
 
 /* normalised chroma sample */
 static inline float csamp(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
-  return (float)rd(in, plane, frame, edge(x, cw), edge(y, ch)) * c->c_scale + c->c_off;
+  const int m = c->p->chroma_edge;
+  return (float)rd(in, plane, frame, edge_m(x, cw, m), edge_m(y, ch, m)) * c->c_scale + c->c_off;
 }
 
 /* horizontal pass (left siting): luma column x from chroma row cy */

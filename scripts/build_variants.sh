@@ -11,7 +11,7 @@ C=$ROOT/hdr-to-sdr_amd/csrc
 O=$ROOT/hdr-to-sdr_amd/build/obj
 V=$ROOT/scripts/variants
 mkdir -p "$V"
-FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed"
+FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed -mllvm -amdgpu-sched-strategy=max-memory-clause"
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}

@@ -200,3 +200,40 @@ def test_gpu_lut_stage_changes_hable_output(kind, seed):
     ys = np.arange(0, H, max(1, H // 20))
     d = np.abs(imgs[0][ys][:, xs] - imgs[1][ys][:, xs])
     assert d.max() >= 30, f'LUT stage changes the Hable output by only {d.max()}/255'
+
+
+# ---- S1 chroma upsampler edge rule (App. B.2) --------------------------------
+@pytest.mark.parametrize('edge', ['zimg', 'replicate', 'mirror'])
+@pytest.mark.parametrize('W,H,extra', [
+    (128, 64, {}),                                   # k_tile only
+    (80, 34, {}),                                    # k_tile + k_process tail (the seam reads column cw)
+    (18, 6, {}),                                     # k_process, ragged group
+    (2, 2, {}),                                      # 1 x 1 chroma planes
+    (128, 64, {'chroma_filter': 'bicubic'}),         # two-pass path
+    (128, 64, {'tonemapper': 'bt.2390'}),            # libplacebo branch on k_tile
+    (192, 32, {'bits_in': 12, 'bits_out': 12, 'transfer': 'arib-std-b67'}),
+])
+def test_chroma_edge_matches_oracle(tm, edge, W, H, extra):
+    kw = dict(tonemapper='hable', gamma=2.2, chroma_edge=edge)
+    kw.update(extra)
+    params = hdr2sdr.TonemapParams(**kw)
+    for kind in ('uniform', 'edges'):
+        got, want, wh = run_both(tm, params, kind, W, H, nframes=2)
+        assert_close_int(params, got, want, *wh)
+
+
+def test_chroma_edge_debug_float_on_tile_path(tm):
+    """The tile kernel's own debug instance reads the border rows through
+    the same rule (stage 1, linear RGB, mirror)."""
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, chroma_edge='mirror')
+    W, H = 128, 64
+    src = synth_frames('uniform', 1, W, H, 10, device='cpu', seed=2)
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    got = tm.debug_float(src.to_torch('cuda'), 1).astype(np.float64)
+    want = oracle.debug_float(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, W, H,
+                              1).astype(np.float64)
+    rows = [0, H - 1]
+    err = np.abs(got[:, rows] - want[:, rows])
+    ok = np.isfinite(want[:, rows]) & (np.abs(want[:, rows]) < 1e6)
+    assert (err[ok] <= 1e-3 * np.abs(want[:, rows][ok]) + 2e-7).all()

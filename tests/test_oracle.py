@@ -272,3 +272,46 @@ def test_multithreaded_oracle_is_deterministic():
     a = oracle.process(p, lattice(), fb.buf, 128, 64, nthreads=1)
     b = oracle.process(p, lattice(), fb.buf, 128, 64, nthreads=4)
     assert np.array_equal(a, b)
+
+
+# ---- S1 chroma upsampler edge rule
+def _edge_out(edge, W=64, H=32):
+    fb = synth_frames('uniform', 1, W, H, 10, seed=12).to_numpy()
+    p = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, chroma_edge=edge)
+    out = oracle.process(oracle.params_from(p.to_c()), lattice(), fb.buf, W, H)
+    o = hdr2sdr.FrameBatch(out, W, H, 10)
+    return o.y[0].astype(int), o.u[0].astype(int), o.v[0].astype(int)
+
+
+def _differs_only_at(a, b, rows, cols):
+    d = a != b
+    d[list(rows), :] = False
+    d[:, list(cols)] = False
+    return not d.any()
+
+
+def test_chroma_edge_rules_act_only_on_the_border():
+    """The bilinear upsampler reads past the chroma plane only for luma rows 0
+    and H-1 (chroma rows -1 / ch) and the last odd luma column (chroma column
+    cw; left siting never reads column -1).  ZIMG and REPLICATE differ at the
+    top only (mirror vs repeat of row -1); ZIMG and MIRROR at the bottom and
+    right only (fold vs mirror of row ch / column cw)."""
+    W, H = 64, 32
+    z, r, m = _edge_out('zimg'), _edge_out('replicate'), _edge_out('mirror')
+    for a, b, rows, cols, crows, ccols in ((z, r, [0], [], [0], []),
+                                          (z, m, [H - 1], [W - 1], [H // 2 - 1], [W // 2 - 1])):
+        assert _differs_only_at(a[0], b[0], rows, cols)
+        assert _differs_only_at(a[1], b[1], crows, ccols) and _differs_only_at(a[2], b[2], crows, ccols)
+        assert any((x != y).any() for x, y in zip(a, b))      # and the rule does change those samples
+
+
+def test_chroma_edge_single_chroma_row_clamps():
+    """1 x 1 chroma planes (2 x 2 luma): every rule stays inside the plane."""
+    outs = [_edge_out(e, 2, 2) for e in ('zimg', 'replicate', 'mirror')]
+    for o in outs[1:]:
+        assert all(np.array_equal(x, y) for x, y in zip(outs[0], o))
+
+
+def test_chroma_edge_rejects_unknown():
+    with pytest.raises(ValueError):
+        hdr2sdr.TonemapParams(chroma_edge='wrap')
