@@ -123,3 +123,28 @@ def test_host_package_never_imports_the_oracle():
         if name.endswith('.py'):
             src = open(os.path.join(pkg, name)).read()
             assert not re.search(r'^\s*(import|from)\s+oracle\b', src, flags=re.M), name
+
+
+def test_integration_stub_matches_the_abi():
+    """INTEGRATION.md's reference-side ctypes stub (the file a maintainer
+    adds as src/h2s_backend.py) loads libh2s and mirrors h2s_params /
+    h2s_frames field for field (h2s_params_default writes the whole C struct
+    into it, so a short mirror would be overwritten past its end)."""
+    import re
+    doc = open(os.path.join(os.path.dirname(HEADER), '..', 'INTEGRATION.md')).read()
+    code = re.search(r'```python\n(# src/h2s_backend.py.*?)```', doc, re.S).group(1)
+    env = dict(os.environ, H2S_LIB=_abi.LIB_PATH)
+    old = os.environ.get('H2S_LIB')
+    os.environ['H2S_LIB'] = env['H2S_LIB']
+    try:
+        ns = {}
+        exec(compile(code, 'INTEGRATION.md', 'exec'), ns)
+    finally:
+        if old is None:
+            del os.environ['H2S_LIB']
+        else:
+            os.environ['H2S_LIB'] = old
+    for mine, ref in ((ns['H2SParams'], _abi.H2SParams), (ns['H2SFrames'], _abi.H2SFrames)):
+        assert ctypes.sizeof(mine) == ctypes.sizeof(ref)
+        assert [(n, getattr(mine, n).offset) for n, _ in mine._fields_] == \
+               [(n, getattr(ref, n).offset) for n, _ in ref._fields_]
