@@ -365,6 +365,9 @@ def main():
     if tr is not None:
         rec['roofline']['traffic'] = tr['bytes_per_dispatch']
         rec['roofline']['traffic_source'] = tr['source']
+        # k_tile's instruction mix from the same PMC passes (per pixel)
+        rec['roofline']['instructions_per_px'] = {k: tr[k] for k in ('valu_per_px', 'trans_per_px', 'cvt_per_px',
+                                                                      'lds_per_px', 'vmem_rd_per_px') if k in tr}
     rec['config']['output_checksum'] = checksum
     if world == 1 and args.cpu_seconds > 0:
         rec['cpu_baseline'] = cpu_baseline(params, lattice_host, W, H, args.cpu_seconds)

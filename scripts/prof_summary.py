@@ -50,6 +50,19 @@ if 'FETCH_SIZE' in vals and 'WRITE_SIZE' in vals:
            'bytes_per_dispatch': int(fs * 2 * 1024 + ws * 1024),
            'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950), KiB->B',
            'dispatches': len(vals['FETCH_SIZE'])}
+    # instruction mix per pixel (wave instructions x 64 lanes / pixels of one dispatch)
+    px = None
+    if workload:
+        import re
+        m = re.search(r'(\d+)x(\d+) .*?(\d+) frames per launch', workload)
+        if m:
+            px = int(m.group(1)) * int(m.group(2)) * int(m.group(3))
+    if px:
+        for key, ctr in (('valu_per_px', 'SQ_INSTS_VALU'), ('trans_per_px', 'SQ_INSTS_VALU_TRANS_F32'),
+                         ('cvt_per_px', 'SQ_INSTS_VALU_CVT'), ('lds_per_px', 'SQ_INSTS_LDS'),
+                         ('vmem_rd_per_px', 'SQ_INSTS_VMEM_RD')):
+            if ctr in vals:
+                rec[key] = round(sum(vals[ctr]) / len(vals[ctr]) * 64 / px, 2)
     with open(os.path.join(d, 'traffic.json'), 'w') as f:
         json.dump(rec, f, indent=1)
     print('traffic.json:', json.dumps(rec))
