@@ -141,6 +141,8 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_INVALID_ARG, "unknown expand");
   if (p->chroma_edge < H2S_EDGE_ZIMG || p->chroma_edge > H2S_EDGE_MIRROR)
     return fail(c, H2S_E_INVALID_ARG, "unknown chroma_edge");
+  if (p->lut_input != H2S_LUT_IN_FLOAT && p->lut_input != H2S_LUT_IN_RGB48)
+    return fail(c, H2S_E_INVALID_ARG, "unknown lut_input");
   if (p->pipeline < H2S_PIPE_AUTO || p->pipeline > H2S_PIPE_LIBPLACEBO)
     return fail(c, H2S_E_INVALID_ARG, "unknown pipeline");
   if (p->pipeline == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
@@ -332,6 +334,7 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   k->dither = p->dither == H2S_DITHER_ORDERED && q == 8 ? 1 : 0;
   k->expand_rep = p->expand == H2S_EXPAND_REPLICATE ? 1 : 0;
   k->chroma_edge = p->chroma_edge;
+  k->lut_in16 = p->lut_input == H2S_LUT_IN_RGB48 && !lp ? 1 : 0;  // the CPU chain's S3 -> S4
   // S7 vf_eq create_lut, generalised to 2^q entries
   const int qn = 1 << q;
   eq->assign(qn, 0);
@@ -891,7 +894,7 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   const h2s_params& p = c->params;
   if (!c->fast_enabled || !k.lut_enabled || !h2s::fast_supported(k.tonemap)) return false;
   if (c->lut_n > 177) return false;
-  if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out)) return false;
+  if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out) || k.lut_in16) return false;
   return true;
 }
 

@@ -59,6 +59,7 @@ struct KParams {
   int eq_identity;
   const uint16_t* eq_lut;
   int chroma_edge;        // S1 upsampler edge rule (chroma_edge_at)
+  int lut_in16;           // S3 -> S4 as 16-bit R'G'B' (h2s_lut_input RGB48)
   int dither;             // ordered 8x8 dither at the 8-bit quantiser
   int expand_rep;         // S8 bit replication instead of a shift
   // Y'CbCr 709 rows
@@ -307,8 +308,9 @@ __device__ __forceinline__ float lut_coord(float x, float lut_max) {
   return __builtin_amdgcn_fmed3f(x * lut_max, 0.0f, lut_max);
 }
 
-__device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g, float& b) {
-  const float sr = lut_coord(r, P.lut_max), sg = lut_coord(g, P.lut_max), sb = lut_coord(b, P.lut_max);
+// tetrahedral blend at lattice coordinates s in [0, N-1] (lut3d interp_tetrahedral)
+__device__ __forceinline__ void lut3d_tetra_at(const KParams& P, float sr, float sg, float sb, float& r, float& g,
+                                               float& b) {
   const int pr = (int)sr, pg = (int)sg, pb = (int)sb;
   const int last = P.lut_n - 1;
   const int str = pr < last ? 1 : 0;
@@ -338,6 +340,10 @@ __device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g
   b = w0 * c000.z + w1 * c1.z + w2 * c2.z + w3 * c111.z;
 }
 
+__device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g, float& b) {
+  lut3d_tetra_at(P, lut_coord(r, P.lut_max), lut_coord(g, P.lut_max), lut_coord(b, P.lut_max), r, g, b);
+}
+
 // libplacebo branch: BT.1886 encode against the target black (oracle lp_encode)
 __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
   x = x > 0.0f ? x : 0.0f;
@@ -349,7 +355,6 @@ __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
 // 8 bits; returns the 8-bit values / 255
 __device__ __forceinline__ float rgba8_q(float v) { return floorf(clamp01(v) * 255.0f + 0.5f); }
 
-__device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g, float& b);
 __device__ __forceinline__ void lut3d_8bit(const KParams& P, float& r, float& g, float& b) {
   const float sf = 1.0f / 255.0f;
   // lut3d_tetra multiplies by lut_max and clips; (q * 1/255) is its input
@@ -359,6 +364,21 @@ __device__ __forceinline__ void lut3d_8bit(const KParams& P, float& r, float& g,
   const float G = fminf(fmaxf(truncf(g * 255.0f), 0.0f), 255.0f);
   const float B = fminf(fmaxf(truncf(b * 255.0f), 0.0f), 255.0f);
   r = R * sf, g = G * sf, b = B * sf;
+}
+
+// S3 -> S4 as 16-bit R'G'B' (h2s_lut_input RGB48; oracle rgb48_q /
+// lut3d_16bit): round to 16 bits, lut3d's 16-bit coordinate, output truncated
+__device__ __forceinline__ float rgb48_q(float v) { return floorf(clamp01(v) * 65535.0f + 0.5f); }
+__device__ __forceinline__ void lut3d_16bit(const KParams& P, float& r, float& g, float& b) {
+  const float scale = (1.0f / 65535.0f) * P.lut_max;
+  const float sr = __builtin_amdgcn_fmed3f(rgb48_q(r) * scale, 0.0f, P.lut_max);
+  const float sg = __builtin_amdgcn_fmed3f(rgb48_q(g) * scale, 0.0f, P.lut_max);
+  const float sb = __builtin_amdgcn_fmed3f(rgb48_q(b) * scale, 0.0f, P.lut_max);
+  float orr, og, ob;
+  lut3d_tetra_at(P, sr, sg, sb, orr, og, ob);
+  r = fminf(fmaxf(truncf(orr * 65535.0f), 0.0f), 65535.0f) / 65535.0f;
+  g = fminf(fmaxf(truncf(og * 65535.0f), 0.0f), 65535.0f) / 65535.0f;
+  b = fminf(fmaxf(truncf(ob * 65535.0f), 0.0f), 65535.0f) / 65535.0f;
 }
 
 // S1 (after upsampling) .. S4 on one pixel.  UPTO = last stage to apply.
@@ -397,6 +417,10 @@ __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, fl
   if (P.lut_enabled) {
     r = bt1886_inv(r), g = bt1886_inv(g), b = bt1886_inv(b);
     if (UPTO == 3) return;
+    if (P.lut_in16) {
+      lut3d_16bit(P, r, g, b);
+      return;
+    }
     lut3d_tetra(P, r, g, b);
   } else {
     float mr = P.m709[0] * r + P.m709[1] * g + P.m709[2] * b;

@@ -32,6 +32,7 @@ CHROMA_BOX, CHROMA_BICUBIC = 0, 1
 DITHER_NONE, DITHER_ORDERED = 0, 1
 EXPAND_SHIFT, EXPAND_REPLICATE = 0, 1
 EDGE_ZIMG, EDGE_REPLICATE, EDGE_MIRROR = 0, 1, 2
+LUT_IN_FLOAT, LUT_IN_RGB48 = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
 OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
@@ -72,7 +73,8 @@ class H2SParams(ctypes.Structure):
         ('target_black', ctypes.c_double),
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 3),
+        ('lut_input', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 2),
     ]
 
 

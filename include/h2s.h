@@ -124,6 +124,13 @@ enum h2s_dither { H2S_DITHER_NONE = 0, H2S_DITHER_ORDERED = 1 };
  * sample.  MIRROR: every edge mirrors about its last sample (ch -> ch-2). */
 enum h2s_chroma_edge { H2S_EDGE_ZIMG = 0, H2S_EDGE_REPLICATE = 1, H2S_EDGE_MIRROR = 2 };
 
+/* Format between S3 and S4 on the CPU chain: which
+ * pixel format ffmpeg negotiates between zscale=t=bt709 and lut3d.  FLOAT:
+ * gbrpf32, lut3d's float path (the round-1 model).  RGB48: 16-bit R'G'B' --
+ * zscale rounds to 16 bits, lut3d's 16-bit path reads q (1/65535) (N-1) and
+ * truncates its output to 16 bits, swscale converts from there. */
+enum h2s_lut_input { H2S_LUT_IN_FLOAT = 0, H2S_LUT_IN_RGB48 = 1 };
+
 /* S8 8-bit -> bits_out expansion after eq. */
 enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
 
@@ -194,7 +201,8 @@ typedef struct h2s_params {
                           * (libplacebo's SDR white, BT.2408), CPU_CHAIN =
                           * npl                                            */
   int32_t chroma_edge;   /* enum h2s_chroma_edge (S1)                       */
-  int32_t reserved[3];
+  int32_t lut_input;     /* enum h2s_lut_input (S3 -> S4, CPU chain)        */
+  int32_t reserved[2];
 } h2s_params;
 
 /* A batch of planar 4:2:0 frames (yuv420p / yuv420p10le / yuv420p12le).

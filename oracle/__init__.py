@@ -49,7 +49,8 @@ class Params(ctypes.Structure):
         ('knee_offset', ctypes.c_double), ('target_black', ctypes.c_double),
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 3),
+        ('lut_input', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 2),
     ]
 
 

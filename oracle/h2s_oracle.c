@@ -430,6 +430,28 @@ static rgbf lut3d_8bit(const ocfg *c, int r8, int g8, int b8) {
   return q;
 }
 
+/* S3 -> S4 as 16-bit R'G'B' (h2s_params.lut_input = RGB48, SURVEY App. B.3;
+ * [EXT], not pinnable here): zimg's float -> word conversion rounds to
+ * nearest; vf_lut3d's 16-bit path scales by (scale / 65535) (N-1) in float and
+ * truncates its output (av_clip_uint16 of the float product's integer
+ * conversion); swscale then reads 16-bit R'G'B' */
+static int rgb48_q(float v) {
+  v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  return (int)floorf(v * 65535.0f + 0.5f);
+}
+
+static rgbf lut3d_16bit(const ocfg *c, int r16, int g16, int b16) {
+  const float lut_max = (float)(c->lut_n - 1), scale = (1.0f / 65535.0f) * lut_max;
+  rgbf s = {clipf((float)r16 * scale, 0, lut_max), clipf((float)g16 * scale, 0, lut_max),
+            clipf((float)b16 * scale, 0, lut_max)};
+  rgbf o = lut3d_tetra_at(c, s);
+  int R = (int)(o.r * 65535.0f), G = (int)(o.g * 65535.0f), B = (int)(o.b * 65535.0f);
+  rgbf q = {(float)(R < 0 ? 0 : (R > 65535 ? 65535 : R)) / 65535.0f,
+            (float)(G < 0 ? 0 : (G > 65535 ? 65535 : G)) / 65535.0f,
+            (float)(B < 0 ? 0 : (B > 65535 ? 65535 : B)) / 65535.0f};
+  return q;
+}
+
 /* ---- one pixel through S1(after upsample)..S4 ---------------------------
  * CPU chain: stage 3 = BT.1886-inverse R'G'B', stage 4 = lut3d output.
  * libplacebo branch: stage 3 = BT.1886 (target black) R'G'B' before the
@@ -484,6 +506,7 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf 
     g.g = bt1886_inverse(t.g);
     g.b = bt1886_inverse(t.b);
     if (upto == H2S_STAGE_GAMMA) return g;
+    if (c->p->lut_input == H2S_LUT_IN_RGB48) return lut3d_16bit(c, rgb48_q(g.r), rgb48_q(g.g), rgb48_q(g.b));
     return lut3d_tetra(c, g);
   }
   rgbf m;

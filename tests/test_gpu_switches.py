@@ -237,3 +237,38 @@ def test_chroma_edge_debug_float_on_tile_path(tm):
     err = np.abs(got[:, rows] - want[:, rows])
     ok = np.isfinite(want[:, rows]) & (np.abs(want[:, rows]) < 1e6)
     assert (err[ok] <= 1e-3 * np.abs(want[:, rows][ok]) + 2e-7).all()
+
+
+# ---- S3 -> S4 format (App. B.3) ----------------------------------------------
+@pytest.mark.parametrize('kw', [dict(tonemapper='hable', gamma=2.2, bits_out=10),
+                                dict(tonemapper='mobius', bits_out=10, mode='native'),
+                                dict(tonemapper='reinhard', bits_out=8),
+                                dict(tonemapper='hable', bits_in=12, bits_out=12, transfer='arib-std-b67')])
+@pytest.mark.parametrize('kind', ['smooth', 'uniform', 'edges'])
+def test_rgb48_lut_input_matches_oracle(tm, kw, kind):
+    params = hdr2sdr.TonemapParams(lut_input='rgb48', **kw)
+    got, want, wh = run_both(tm, params, kind, 128, 64)
+    assert_close_int(params, got, want, *wh)
+    assert _path(tm, params, 128, 64) == _abi.PATH_GENERIC      # the tile kernel models the float path only
+
+
+def test_rgb48_debug_stage4_matches_oracle(tm):
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, lut_input='rgb48')
+    W, H = 128, 64
+    src = synth_frames('smooth', 1, W, H, 10, device='cpu', seed=6)
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    got = tm.debug_float(src.to_torch('cuda'), 4).astype(np.float64)
+    want = oracle.debug_float(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, W, H,
+                              4).astype(np.float64)
+    d = np.abs(got - want)
+    # both are k / 65535.  Where all four corners are exactly 1.0 (the gamut
+    # clip saturates large parts of the lattice) the blend is 1.0 or
+    # 0.99999994 depending on FMA contraction (fused on the GPU, separate on
+    # the oracle's x86 build) and lut3d's truncation maps that to 65535 or
+    # 65534: one 16-bit step, invisible after the 8/10-bit quantiser.  A flip
+    # of the 16-bit input rounding (an ulp of the GPU's vs libm's powf next to
+    # a rounding boundary) moves the coordinate by (N-1)/65535 and the value by
+    # a few steps (~2 % of values here).  The 1e-3 float bound holds for all.
+    assert (d <= 1e-3 * np.abs(want) + 6e-4).all()
+    assert (d < 1.5 / 65535).mean() > 0.95

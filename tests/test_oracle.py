@@ -315,3 +315,31 @@ def test_chroma_edge_single_chroma_row_clamps():
 def test_chroma_edge_rejects_unknown():
     with pytest.raises(ValueError):
         hdr2sdr.TonemapParams(chroma_edge='wrap')
+
+
+# ---- S3 -> S4 format -----------------
+def test_rgb48_lut_input_is_a_small_perturbation_of_the_float_path():
+    """16-bit R'G'B' between zscale and lut3d (rounding in, truncation out, both
+    at 1/65535) moves the quantised output by at most one step, on a small
+    fraction of samples -- but it does move it (the switch is live)."""
+    W, H = 128, 64
+    fb = synth_frames('smooth', 2, W, H, 10, seed=13).to_numpy()
+    base = hdr2sdr.TonemapParams(tonemapper='hable', gamma=1.0, bits_out=10, mode='native')  # no eq: steps stay steps
+    outs = [oracle.process(oracle.params_from(p.to_c()), lattice(), fb.buf, W, H).astype(int)
+            for p in (base, base.with_(lut_input='rgb48'))]
+    d = np.abs(outs[0] - outs[1])
+    assert d.max() <= 1 and 0 < (d > 0).mean() < 0.05
+
+
+def test_rgb48_lut_stage_values_are_16bit():
+    W, H = 64, 32
+    fb = synth_frames('ramp', 1, W, H, 10, seed=2).to_numpy()
+    p = hdr2sdr.TonemapParams(tonemapper='hable', lut_input='rgb48')
+    st4 = oracle.debug_float(oracle.params_from(p.to_c()), lattice(), fb.buf, W, H, 4).astype(np.float64)
+    q = st4 * 65535.0
+    assert np.allclose(q, np.round(q), atol=2e-3) and st4.min() >= 0 and st4.max() <= 1
+
+
+def test_lut_input_rejects_unknown():
+    with pytest.raises(ValueError):
+        hdr2sdr.TonemapParams(lut_input='rgb24')
