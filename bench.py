@@ -33,8 +33,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    # 1000 launches of 64 4K frames: a ~2 s timed region, long enough for an
+    # outside sampler (rocm-smi) to see the GPU busy; kernel_ms averages the
+    # last 256 launches (the context's event ring)
+    ap.add_argument('--steps', type=int, default=1000)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--frames', type=int, default=64,
                     help='frames per rank per step (C4: 512 frames / 8 GPUs = 64)')
     ap.add_argument('--width', type=int, default=3840)
