@@ -530,7 +530,9 @@ void h2s_params_default(h2s_params* p) {
   p->gamma = 1.0;
   p->lut_enabled = 1;
   p->mode = H2S_MODE_COMPAT8;
-  p->desat_luma = H2S_DESAT_LUMA_RGB;
+  // App. B.1 settled by the reference's own website pair (tests/test_website_fixture.py):
+  // weighted luma fits its SDR frame 3-4/255 better than the {1,1,1} RGB entry
+  p->desat_luma = H2S_DESAT_LUMA_BT2020;
   // [EXT] switches: the round-1 models; pipeline AUTO; libplacebo targets from the branch
   p->chroma_filter = H2S_CHROMA_BOX;
   p->dither = H2S_DITHER_NONE;
@@ -718,7 +720,6 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->lr = k.lr, F->lg = k.lg, F->lb = k.lb, F->desat = k.desat;
   F->rein_p = k.rein_p, F->rein_k = k.rein_k;
   F->hable_peak_inv = k.hable_peak_inv;
-  F->hable_ef_peak_inv = (0.02f / 0.30f) * k.hable_peak_inv;
   F->hable_ka = (float)(2.1 / 15.0 * (double)k.hable_peak_inv);
   F->hable_kb = (float)(0.25 / 15.0 * (double)k.hable_peak_inv);
   F->mob_j = k.mob_j, F->mob_a = k.mob_a, F->mob_b = k.mob_b, F->mob_k = k.mob_k;

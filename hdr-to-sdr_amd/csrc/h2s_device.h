@@ -117,7 +117,7 @@ struct FastParams : CurveConsts {
   // S2
   float lr, lg, lb, desat;
   float rein_p, rein_k;
-  float hable_peak_inv, hable_ef_peak_inv;
+  float hable_peak_inv;
   float hable_ka, hable_kb;        // 0.14 / hable(peak), (1/60) / hable(peak): hable(x)/x = (0.14 x + 1/60) / D(x)
   float mob_j, mob_a, mob_b, mob_k;
   float npl_1e4, e4_npl;

@@ -191,31 +191,32 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
       s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
     }
-    const float k = s2 * frcp(sig);
+    const float k = safe ? s2 / sig : s2 * frcp(sig);   // IEEE division on the exact path (see below)
     r *= k, g *= k, b *= k;
     return;
   }
   if (safe) {
+    // the wave met the exact PQ path: linear values up to ~1e38 or inf.
+    // vf_tonemap's statement order with IEEE division, as the generic kernel
+    // (tonemap_px): v_rcp_f32 flushes the (denormal) reciprocal of anything
+    // above 8.5e37 to zero, which Hable's num/den reaches at sig ~ 2.7e19
     if (DESAT) {
       const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
-      const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
-      const float iob = 1.0f - ob;
-      r = r * iob + luma * ob;
-      g = g * iob + luma * ob;
-      b = b * iob + luma * ob;
+      const float ob = fmaxf(luma - F.desat, 1e-6f) / fmaxf(luma, 1e-6f);
+      r = r * (1.0f - ob) + luma * ob;
+      g = g * (1.0f - ob) + luma * ob;
+      b = b * (1.0f - ob) + luma * ob;
     }
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-    float k;
-    if (TM == 4) {  // REINHARD: sig/(sig+p) * (peak+p)/peak
-      k = F.rein_k * frcp(sig + F.rein_p);
-    } else if (TM == 5) {  // HABLE: hable(sig) / hable(peak)
-      const float num = sig * (sig * 0.15f + 0.05f) + 0.004f;
-      const float den = sig * (sig * 0.15f + 0.50f) + 0.06f;
-      k = fmaf(num * frcp(den), F.hable_peak_inv, -F.hable_ef_peak_inv) * frcp(sig);
+    float t;
+    if (TM == 4) {  // REINHARD
+      t = sig / (sig + F.rein_p) * F.rein_k;
+    } else if (TM == 5) {  // HABLE
+      t = hable(sig) * F.hable_peak_inv;
     } else {  // MOBIUS: identity below j
-      const float m = F.mob_k * (sig + F.mob_a) * frcp(sig + F.mob_b) * frcp(sig);
-      k = sig <= F.mob_j ? 1.0f : m;
+      t = sig <= F.mob_j ? sig : F.mob_k * (sig + F.mob_a) / (sig + F.mob_b);
     }
+    const float k = t / sig;
     r *= k, g *= k, b *= k;
     return;
   }
