@@ -530,9 +530,7 @@ void h2s_params_default(h2s_params* p) {
   p->gamma = 1.0;
   p->lut_enabled = 1;
   p->mode = H2S_MODE_COMPAT8;
-  // App. B.1 settled by the reference's own website pair (tests/test_website_fixture.py):
-  // weighted luma fits its SDR frame 3-4/255 better than the {1,1,1} RGB entry
-  p->desat_luma = H2S_DESAT_LUMA_BT2020;
+  p->desat_luma = H2S_DESAT_LUMA_RGB;
   // [EXT] switches: the round-1 models; pipeline AUTO; libplacebo targets from the branch
   p->chroma_filter = H2S_CHROMA_BOX;
   p->dither = H2S_DITHER_NONE;

@@ -87,7 +87,7 @@ class TonemapParams:
     npl: float = 100.0
     maxcll: float = 0.0
     mastering_max: float = 0.0
-    desat_luma: str = 'bt2020'  # App. B.1: weighted luma (tests/test_website_fixture.py)
+    desat_luma: str = 'rgb'
     peak_detect: bool = False   # BT.2390 / spline: detected, smoothed per-frame peak (libplacebo peak_detect=1)
     chroma_filter: str = 'box'  # S6 4:4:4 -> 4:2:0 ('box' | 'bicubic')
     dither: str = 'none'        # 8-bit quantiser ('none' | 'ordered')

@@ -79,13 +79,11 @@ enum h2s_tonemap {
 enum h2s_mode { H2S_MODE_COMPAT8 = 0, H2S_MODE_NATIVE = 1 };
 
 /* Luma weights tonemap's desaturation uses: vf_tonemap reads the frame's
- * colorspace tag, which the first zscale (no m=) carries through as
- * bt2020nc -- or, if colorspace negotiation retagged the float RGB frame, the
- * libavutil RGB entry {1,1,1}.  Default BT2020: on
- * the reference's own website pair (hdr-frame.png -> sdr-frame.png) weighted
- * luma reproduces the SDR frame to 4.4/255 mean abs error at its best-fit
- * peak, {1,1,1} to 7.5/255 at best (tests/test_website_fixture.py).  BT2020,
- * BT709 and desat off are indistinguishable there. */
+ * colorspace tag -- bt2020nc if the first zscale (no m=) carries it through,
+ * or, if colorspace negotiation retags the float RGB frame, the libavutil RGB
+ * entry {1,1,1} (the default).  Switchable because it cannot be pinned
+ * without the bundled ffmpeg: the reference's only
+ * pixel pair was made on its libplacebo branch, where no vf_tonemap runs. */
 enum h2s_desat_luma {
   H2S_DESAT_LUMA_RGB = 0,    /* {1, 1, 1}                 */
   H2S_DESAT_LUMA_BT2020 = 1, /* {0.2627, 0.6780, 0.0593}  */

@@ -78,7 +78,7 @@ def default_params(**kw) -> Params:
     """Reference chain defaults (see include/h2s.h h2s_params_default)."""
     p = Params(transfer_in=0, bits_in=10, bits_out=10, tonemap=6, tm_param=math.nan,
                desat=2.0, peak=0.0, npl=100.0, gamma=1.0, maxcll=0.0, mastering_max=0.0,
-               lut_enabled=1, mode=0, desat_luma=1, knee_offset=math.nan, target_black=math.nan,
+               lut_enabled=1, mode=0, desat_luma=0, knee_offset=math.nan, target_black=math.nan,
                target_white=math.nan)
     for k, v in kw.items():
         setattr(p, k, v)
