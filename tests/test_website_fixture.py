@@ -21,7 +21,11 @@ What this pins (PARITY otherwise UNPINNED: libplacebo is absent):
 * the SDR target white: the same curve against a 100-nit white misses by
   5.8/255 at its best peak (about 1700 nits), vf_tonemap's BT.2390 (the CPU
   chain's form: npl 100, no black lift) by 7.2/255 at its best;
+* libplacebo's black-point lift (target black = white/1000): without it the
+  best fit is 4.2/255;
 * the branch: none of the CPU chain's vf_tonemap curves gets within 1/255 of it.
+Not settled by it: knee offset 1.0 vs the ITU 0.5 (3.09 vs 3.15/255 at
+their best peaks) and LUT on vs off (3.09 vs 2.99/255).
 """
 import os
 
@@ -80,6 +84,12 @@ def test_sdr_white_target_is_203_nits():
     best = min(mae_oracle(fb, sdr, tonemapper='bt.2390', peak=p) for p in PEAKS)
     for other in (dict(target_white=100.0), dict(pipeline='cpu')):
         assert min(mae_oracle(fb, sdr, tonemapper='bt.2390', peak=p, **other) for p in PEAKS) > best + 2.5
+
+
+def test_black_point_lift():
+    fb, sdr = fixture_frame()
+    best = min(mae_oracle(fb, sdr, tonemapper='bt.2390', peak=p) for p in PEAKS)
+    assert min(mae_oracle(fb, sdr, tonemapper='bt.2390', peak=p, target_black=0.0) for p in PEAKS) > best + 0.8
 
 
 def test_no_cpu_chain_curve_matches_it():
