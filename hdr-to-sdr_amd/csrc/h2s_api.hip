@@ -145,6 +145,8 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_INVALID_ARG, "unknown lut_input");
   if (p->pipeline < H2S_PIPE_AUTO || p->pipeline > H2S_PIPE_LIBPLACEBO)
     return fail(c, H2S_E_INVALID_ARG, "unknown pipeline");
+  if (p->lp_tone != H2S_LP_TONE_IPT && p->lp_tone != H2S_LP_TONE_MAX_RGB)
+    return fail(c, H2S_E_INVALID_ARG, "unknown lp_tone");
   if (p->pipeline == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
     return fail(c, H2S_E_UNSUPPORTED,
                 "libplacebo pipeline: only bt.2390 / spline are restated (libplacebo's hable/mobius/reinhard "
@@ -232,6 +234,44 @@ double pq_eotf_d(double e) {
   return pow(num / (c2 - c3 * xp), 1.0 / m1);
 }
 
+// IPT-PQ matrices (h2s_lp_tone IPT), built in double and rounded once:
+// BT.2020 RGB -> XYZ from the primaries and D65 white, XYZ -> LMS by the
+// Hunt-Pointer-Estevez matrix of IPT (D65-normalised: neutral L = M = S = Y),
+// the inverse, and the inverse of the Ebner-Fairchild L'M'S' -> IPT matrix
+// (its I column is exactly 1: the P and T rows sum to 0)
+static void inv3(const double m[3][3], double o[3][3]) {
+  const double d = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                   m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      o[i][j] = (m[(j + 1) % 3][(i + 1) % 3] * m[(j + 2) % 3][(i + 2) % 3] -
+                 m[(j + 1) % 3][(i + 2) % 3] * m[(j + 2) % 3][(i + 1) % 3]) / d;
+}
+
+static void ipt_matrices(float r2l[9], float l2r[9], float i2l[9]) {
+  const double prim[3][2] = {{0.708, 0.292}, {0.170, 0.797}, {0.131, 0.046}}, wx = 0.3127, wy = 0.3290;
+  double xyz[3][3], xyzi[3][3];
+  for (int k = 0; k < 3; k++) {
+    xyz[0][k] = prim[k][0] / prim[k][1];
+    xyz[1][k] = 1.0;
+    xyz[2][k] = (1.0 - prim[k][0] - prim[k][1]) / prim[k][1];
+  }
+  inv3(xyz, xyzi);
+  const double w[3] = {wx / wy, 1.0, (1.0 - wx - wy) / wy};
+  for (int k = 0; k < 3; k++) {
+    const double sk = xyzi[k][0] * w[0] + xyzi[k][1] * w[1] + xyzi[k][2] * w[2];
+    for (int i = 0; i < 3; i++) xyz[i][k] *= sk;                       // RGB -> XYZ
+  }
+  const double hpe[3][3] = {{0.4002, 0.7076, -0.0808}, {-0.2263, 1.1653, 0.0457}, {0.0, 0.0, 0.9182}};
+  const double ipt[3][3] = {{0.4, 0.4, 0.2}, {4.455, -4.851, 0.396}, {0.8056, 0.3572, -1.1628}};
+  double rl[3][3], lr[3][3], il[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) rl[i][k] = hpe[i][0] * xyz[0][k] + hpe[i][1] * xyz[1][k] + hpe[i][2] * xyz[2][k];
+  inv3(rl, lr);
+  inv3(ipt, il);
+  for (int i = 0; i < 9; i++) r2l[i] = (float)rl[i / 3][i % 3], l2r[i] = (float)lr[i / 3][i % 3], i2l[i] = (float)il[i / 3][i % 3];
+}
+
 void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   memset(k, 0, sizeof(*k));
   // S1 zimg: depth conversion (limited range), BT.2020-NCL matrix, scale
@@ -302,6 +342,8 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
                                                                                                       : h2s::PIPE_CPU);
   const bool lp = k->pipe == h2s::PIPE_LIBPLACEBO;
   k->rgba8 = lp && p->lut_enabled ? 1 : 0;
+  k->lp_ipt = lp && p->lp_tone == H2S_LP_TONE_IPT ? 1 : 0;
+  ipt_matrices(k->ipt_r2l, k->ipt_l2r, k->ipt_i2l);
   k->t_white = isnan(p->target_white) ? (lp ? 203.0 : p->npl) : p->target_white;
   k->t_black = isnan(p->target_black) ? (lp ? k->t_white / 1000.0 : 0.0) : p->target_black;
   k->knee_off = isnan(p->knee_offset) ? 1.0 : p->knee_offset;
@@ -539,6 +581,9 @@ void h2s_params_default(h2s_params* p) {
   p->knee_offset = NAN;
   p->target_black = NAN;
   p->target_white = NAN;
+  p->chroma_edge = H2S_EDGE_ZIMG;
+  p->lut_input = H2S_LUT_IN_FLOAT;
+  p->lp_tone = H2S_LP_TONE_IPT;   // libplacebo >= 6 tone-maps in IPT (h2s.h enum h2s_lp_tone)
 }
 
 int h2s_create(int device, h2s_ctx** out) {
@@ -733,6 +778,9 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->qscale = k.qscale;
   F->c56 = 56.0f * k.qscale;
   for (int i = 0; i < 3; i++) F->k709[i] = k.k709[i], F->kcb[i] = k.kcb[i], F->kcr[i] = k.kcr[i];
+  F->lp_ipt = k.lp_ipt;
+  for (int i = 0; i < 9; i++) F->ipt_r2l[i] = (float)((double)k.ipt_r2l[i] * (double)k.npl_1e4), F->ipt_l2r[i] = k.ipt_l2r[i];
+  for (int i = 0; i < 3; i++) F->ipt_pt[2 * i] = k.ipt_i2l[3 * i + 1], F->ipt_pt[2 * i + 1] = k.ipt_i2l[3 * i + 2];
   curve_fast(k, F);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));

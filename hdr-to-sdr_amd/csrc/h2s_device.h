@@ -48,6 +48,8 @@ struct KParams {
   // pipeline (h2s_pipeline, resolved to CPU_CHAIN or LIBPLACEBO)
   int pipe, rgba8;
   float enc_ainv, enc_b;  // libplacebo BT.1886 encode: (x * ainv)^(1/2.4) - b
+  int lp_ipt;             // libplacebo branch: the curve on IPT-PQ intensity (h2s_lp_tone IPT)
+  float ipt_r2l[9], ipt_l2r[9], ipt_i2l[9];  // BT.2020 RGB -> LMS, inverse; IPT -> L'M'S' (row-major)
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
   float lut_max;
@@ -128,6 +130,10 @@ struct FastParams : CurveConsts {
   // lut3d's 8-bit coordinate (q * inv255) * nm1; BT.709 rows at depth q
   float lp_k1, lp_k2, lp_xmax, nm1, inv255, qscale, c56;
   float k709[3], kcb[3], kcr[3];
+  // lp_tone = IPT: RGB (npl units) -> LMS / 10000 (npl/10000 folded in); LMS
+  // -> RGB; the P and T columns of IPT -> L'M'S' (the I column is 1)
+  int lp_ipt;
+  float ipt_r2l[9], ipt_l2r[9], ipt_pt[6];
   const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
@@ -231,9 +237,50 @@ __device__ __forceinline__ float bt2390_black(float mn, float bp, float gain, fl
   return gain * (x - mn) + mn;
 }
 
+// libplacebo bt2390 on a PQ-domain signal (oracle bt2390_pq)
+__device__ __forceinline__ float bt2390_pq(const KParams& P, float e1) {
+  float e1n = (e1 - P.b_srcmin) * P.b_inv_range;
+  e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);  // clip to the source range (NaN -> 1)
+  float e2 = e1n;
+  if (P.b_ks < 1.0f && e1n > P.b_ks) {
+    float t = (e1n - P.b_ks) * P.b_inv_1mks;
+    float t2 = t * t, t3 = t2 * t;
+    e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * P.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - P.b_ks) +
+         (-2.0f * t3 + 3.0f * t2) * P.b_maxlum;
+  }
+  e2 = bt2390_black(P.b_minlum, P.b_bp, P.b_gain, e2);
+  return e2 * P.b_range + P.b_srcmin;
+}
+
+// libplacebo branch, h2s_lp_tone IPT (oracle tone_ipt): the PQ-domain curve
+// on the intensity of IPT-PQ, P and T kept; linear in, linear out (units of
+// npl in, of the target white out)
+__device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, float& b) {
+  const float s = P.npl_1e4;
+  const float v0 = fminf(r, 1e6f) * s, v1 = fminf(g, 1e6f) * s, v2 = fminf(b, 1e6f) * s;
+  float q[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) q[k] = pq_encode(P.ipt_r2l[3 * k] * v0 + P.ipt_r2l[3 * k + 1] * v1 + P.ipt_r2l[3 * k + 2] * v2);
+  const float I = 0.4f * q[0] + 0.4f * q[1] + 0.2f * q[2];
+  const float Pc = 4.455f * q[0] - 4.851f * q[1] + 0.396f * q[2];
+  const float T = 0.8056f * q[0] + 0.3572f * q[1] - 1.1628f * q[2];
+  const float I2 = P.tonemap == 8 ? spline_pq(P, I) : bt2390_pq(P, I);
+  float l[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) l[k] = pq_eotf(I2 + P.ipt_i2l[3 * k + 1] * Pc + P.ipt_i2l[3 * k + 2] * T);
+  const float os = P.e4_npl;
+  r = (P.ipt_l2r[0] * l[0] + P.ipt_l2r[1] * l[1] + P.ipt_l2r[2] * l[2]) * os;
+  g = (P.ipt_l2r[3] * l[0] + P.ipt_l2r[4] * l[1] + P.ipt_l2r[5] * l[2]) * os;
+  b = (P.ipt_l2r[6] * l[0] + P.ipt_l2r[7] * l[1] + P.ipt_l2r[8] * l[2]) * os;
+}
+
 // S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)
 __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g, float& b) {
   float sig, sig_orig;
+  if (P.lp_ipt && (P.tonemap == 7 || P.tonemap == 8)) {
+    tone_ipt(P, r, g, b);
+    return;
+  }
   if (P.tonemap == 8 /* SPLINE */) {
     sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     const float s2 = pq_eotf(spline_pq(P, pq_encode(sig * P.npl_1e4))) * P.e4_npl;
@@ -243,17 +290,7 @@ __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g,
   }
   if (P.tonemap == 7 /* BT2390 */) {
     sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
-    float e1n = (pq_encode(sig * P.npl_1e4) - P.b_srcmin) * P.b_inv_range;
-    e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);  // clip to the source range (NaN -> 1)
-    float e2 = e1n;
-    if (P.b_ks < 1.0f && e1n > P.b_ks) {
-      float t = (e1n - P.b_ks) * P.b_inv_1mks;
-      float t2 = t * t, t3 = t2 * t;
-      e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * P.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - P.b_ks) +
-           (-2.0f * t3 + 3.0f * t2) * P.b_maxlum;
-    }
-    e2 = bt2390_black(P.b_minlum, P.b_bp, P.b_gain, e2);
-    float s2 = pq_eotf(e2 * P.b_range + P.b_srcmin) * P.e4_npl;
+    float s2 = pq_eotf(bt2390_pq(P, pq_encode(sig * P.npl_1e4))) * P.e4_npl;
     float k = s2 / sig;
     r *= k, g *= k, b *= k;
     return;

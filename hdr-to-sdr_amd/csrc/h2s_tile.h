@@ -133,23 +133,17 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // sig = max(R,G,B) back to PQ, and PQ(EOTF(max E)) = max E, so e1 is the
 // input's own max code value (emax_s = max E * PQ_SEG + 1, clamped below at
 // the code of sig = 1e-6); the final decode reads the EOTF table in LDS.
+// libplacebo branch with h2s_lp_tone IPT (F.lp_ipt): the curve acts on the
+// intensity of IPT-PQ instead (three exact PQ encodes of the LMS rows, three
+// table decodes of L'M'S' = I' + a P + b T), as the oracle's tone_ipt.
 template <int TRC, int TM, int DESAT>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds, float& r,
                                      float& g, float& b, bool safe, float emax_s) {
   if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
-    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
-    float e1;
-    if (TRC == 0 && !safe) {
-      e1 = fmaxf(fmaf(emax_s, 1.0f / (float)PQ_SEG, -1.0f / (float)PQ_SEG), F.b_e1min);
-    } else {  // exact PQ encode: HLG input, or the wave met the exact EOTF path
-      const float ym = fexp2(flog2(sig * F.npl_1e4) * PQ_M1);
-      e1 = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
-    }
-    float s2;
-    if (TRC == 0) {
-      // the curve straight into pq_z's table coordinate u = e4*PQ_SEG + 1:
-      // the output scale and offset are folded into the polynomial
-      // coefficients on the host (resolve_fast)
+    // PQ input: the curve straight into pq_z's table coordinate u = e4*PQ_SEG
+    // + 1 (the output scale and offset are folded into the polynomial
+    // coefficients on the host, resolve_fast)
+    auto curve_u = [&](float e1) -> float {
       float u;
       if (TM == 7) {   // BT.2390 Hermite knee as one cubic in t, Horner form
         const float e1n = __builtin_amdgcn_fmed3f(fmaf(e1, C.b_e1a, C.b_e1b), 0.0f, 1.0f);
@@ -174,9 +168,10 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
         const float up = fmaf(fmaf(C.sp_pa_u, x, C.sp_pb_u), x, C.sp_k_u);
         u = __builtin_amdgcn_fmed3f(x > 0.0f ? uq : up, C.sp_umin, C.sp_umax);
       }
-      s2 = pq_z(pq_lds, u) * F.tw_fold;                           // EOTF(e4) * 10000/target white
-    } else {
-      float e4;
+      return u;
+    };
+    // HLG input: the curve's PQ output e4
+    auto curve_e4 = [&](float e1) -> float {
       if (TM == 7) {
         const float e1n = fmaxf(fminf((e1 - C.b_srcmin) * C.b_inv_range, 1.0f), 0.0f);
         const float t = (e1n - C.b_ks) * C.b_inv_1mks;
@@ -184,13 +179,59 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
         const float p = (2.0f * t3 - 3.0f * t2 + 1.0f) * C.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - C.b_ks) +
                         (-2.0f * t3 + 3.0f * t2) * C.b_maxlum;
         const float e2 = bt2390_black(C.b_minlum, C.b_bp, C.b_gain, (C.b_ks < 1.0f && e1n > C.b_ks) ? p : e1n);
-        e4 = fmaxf(e2 * C.b_range + C.b_srcmin, 0.0f);   // <= source max <= 1
-      } else {
-        e4 = spline_pq(C, e1);                            // within [PQ(0), PQ(npl)]
+        return fmaxf(e2 * C.b_range + C.b_srcmin, 0.0f);   // <= source max <= 1
       }
-      const float xp = fexp2(flog2(e4) * (1.0f / PQ_M2));
-      s2 = fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1)) * F.e4_npl;
+      return spline_pq(C, e1);                              // within [PQ(0), PQ(npl)]
+    };
+    auto eotf_exact = [](float e) -> float {   // normalised (1 = 10000 nits), e in [0, ~1.1]
+      const float xp = fexp2(flog2(fmaxf(e, 0.0f)) * (1.0f / PQ_M2));
+      return fexp2(flog2(fmaxf(xp - PQ_C1, 0.0f) * frcp(PQ_C2 - PQ_C3 * xp)) * (1.0f / PQ_M1));
+    };
+    auto pq_enc = [](float y) -> float {       // y = luminance / 10000
+      const float ym = fexp2(flog2(fmaxf(y, 0.0f)) * PQ_M1);
+      return fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
+    };
+    if (F.lp_ipt) {
+      // libplacebo branch, h2s_lp_tone IPT (oracle tone_ipt): the curve on
+      // the intensity of IPT-PQ, P and T kept (launch-uniform branch)
+      const float R = fminf(r, 1e6f), G = fminf(g, 1e6f), B = fminf(b, 1e6f);
+      const float q0 = pq_enc(F.ipt_r2l[0] * R + F.ipt_r2l[1] * G + F.ipt_r2l[2] * B);
+      const float q1 = pq_enc(F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
+      const float q2 = pq_enc(F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
+      const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
+      const float Pc = 4.455f * q0 - 4.851f * q1 + 0.396f * q2;
+      const float T = 0.8056f * q0 + 0.3572f * q1 - 1.1628f * q2;
+      float l0, l1, l2, os;
+      if (TRC == 0) {   // L' = I' + a P + b T on the EOTF table's coordinate
+        const float u = curve_u(I);
+        const float ps = Pc * (float)PQ_SEG, ts = T * (float)PQ_SEG;
+        auto lz = [&](int k) {
+          return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(F.ipt_pt[2 * k], ps, fmaf(F.ipt_pt[2 * k + 1], ts, u)), 1.0f,
+                                                      PQZ_LIM - 0.01f));
+        };
+        l0 = lz(0), l1 = lz(1), l2 = lz(2);
+        os = F.tw_fold;
+      } else {
+        const float e4 = curve_e4(I);
+        l0 = eotf_exact(e4 + F.ipt_pt[0] * Pc + F.ipt_pt[1] * T);
+        l1 = eotf_exact(e4 + F.ipt_pt[2] * Pc + F.ipt_pt[3] * T);
+        l2 = eotf_exact(e4 + F.ipt_pt[4] * Pc + F.ipt_pt[5] * T);
+        os = F.e4_npl;
+      }
+      r = (F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2) * os;
+      g = (F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2) * os;
+      b = (F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2) * os;
+      return;
     }
+    const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
+    float e1;
+    if (TRC == 0 && !safe) {
+      e1 = fmaxf(fmaf(emax_s, 1.0f / (float)PQ_SEG, -1.0f / (float)PQ_SEG), F.b_e1min);
+    } else {  // exact PQ encode: HLG input, or the wave met the exact EOTF path
+      e1 = pq_enc(sig * F.npl_1e4);
+    }
+    // EOTF(e4) * 10000/target white (TRC 0: the table is npl-scaled)
+    const float s2 = TRC == 0 ? pq_z(pq_lds, curve_u(e1)) * F.tw_fold : eotf_exact(curve_e4(e1)) * F.e4_npl;
     const float k = safe ? s2 / sig : s2 * frcp(sig);   // IEEE division on the exact path (see below)
     r *= k, g *= k, b *= k;
     return;

@@ -33,6 +33,7 @@ DITHER_NONE, DITHER_ORDERED = 0, 1
 EXPAND_SHIFT, EXPAND_REPLICATE = 0, 1
 EDGE_ZIMG, EDGE_REPLICATE, EDGE_MIRROR = 0, 1, 2
 LUT_IN_FLOAT, LUT_IN_RGB48 = 0, 1
+LP_TONE_IPT, LP_TONE_MAX_RGB = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
 OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
@@ -74,7 +75,7 @@ class H2SParams(ctypes.Structure):
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
         ('lut_input', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 2),
+        ('lp_tone', ctypes.c_int32), ('reserved', ctypes.c_int32 * 1),
     ]
 
 

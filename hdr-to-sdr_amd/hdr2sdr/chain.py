@@ -58,6 +58,7 @@ _EXPAND = {'shift': _abi.EXPAND_SHIFT, 'replicate': _abi.EXPAND_REPLICATE}
 # which of the reference's two chains: 'auto' = libplacebo for the GPU-only
 # operators (the only chain that has them), the CPU chain otherwise
 _LUT_IN = {'float': _abi.LUT_IN_FLOAT, 'rgb48': _abi.LUT_IN_RGB48}
+_LP_TONE = {'ipt': _abi.LP_TONE_IPT, 'max-rgb': _abi.LP_TONE_MAX_RGB}
 _EDGE = {'zimg': _abi.EDGE_ZIMG, 'replicate': _abi.EDGE_REPLICATE, 'mirror': _abi.EDGE_MIRROR}
 _PIPELINE = {'auto': _abi.PIPE_AUTO, 'cpu': _abi.PIPE_CPU_CHAIN, 'libplacebo': _abi.PIPE_LIBPLACEBO}
 
@@ -98,6 +99,7 @@ class TonemapParams:
     target_white: float = math.nan  # SDR target white, nits (NaN: libplacebo 203, CPU chain npl)
     chroma_edge: str = 'zimg'   # S1 upsampler edge rule ('zimg' | 'replicate' | 'mirror')
     lut_input: str = 'float'    # S3 -> S4 format on the CPU chain ('float' | 'rgb48')
+    lp_tone: str = 'ipt'        # libplacebo branch: curve on IPT intensity | gain on max(R,G,B) ('ipt' | 'max-rgb')
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
@@ -110,7 +112,7 @@ class TonemapParams:
         if self.desat_luma not in _DESAT_LUMA:
             raise ValueError(f'unknown desat_luma {self.desat_luma!r}')
         for name, table in (('chroma_filter', _CHROMA), ('dither', _DITHER), ('expand', _EXPAND),
-                            ('pipeline', _PIPELINE), ('chroma_edge', _EDGE), ('lut_input', _LUT_IN)):
+                            ('pipeline', _PIPELINE), ('chroma_edge', _EDGE), ('lut_input', _LUT_IN), ('lp_tone', _LP_TONE)):
             if getattr(self, name) not in table:
                 raise ValueError(f'unknown {name} {getattr(self, name)!r}; expected one of {sorted(table)}')
         if self.pipeline == 'libplacebo' and tm not in GPU_ONLY_TONEMAPPERS:
@@ -175,6 +177,7 @@ class TonemapParams:
         p.target_white = self.target_white
         p.chroma_edge = _EDGE[self.chroma_edge]
         p.lut_input = _LUT_IN[self.lut_input]
+        p.lp_tone = _LP_TONE[self.lp_tone]
         return p
 
     def resolved_pipeline(self) -> str:

@@ -133,6 +133,16 @@ enum h2s_chroma_edge { H2S_EDGE_ZIMG = 0, H2S_EDGE_REPLICATE = 1, H2S_EDGE_MIRRO
  * truncates its output to 16 bits, swscale converts from there. */
 enum h2s_lut_input { H2S_LUT_IN_FLOAT = 0, H2S_LUT_IN_RGB48 = 1 };
 
+/* How the libplacebo branch applies its PQ-domain curve (BT.2390 / SPLINE)
+ * to colour.  libplacebo is absent: PARITY UNPINNED.  IPT (default): the
+ * curve maps the intensity I of IPT-PQ -- linear BT.2020 -> XYZ -> LMS
+ * (Hunt-Pointer-Estevez, D65-normalised), PQ-encoded in absolute
+ * luminance, I = 0.4 L' + 0.4 M' + 0.2 S' (Ebner-Fairchild) -- and keeps
+ * P and T; libplacebo tone-maps in IPT since v6, and on the reference's own
+ * before/after pair this fits best (tests/test_website_fixture.py).
+ * MAX_RGB: gain curve(max RGB) / max RGB on R, G, B (the round-2 model). */
+enum h2s_lp_tone { H2S_LP_TONE_IPT = 0, H2S_LP_TONE_MAX_RGB = 1 };
+
 /* S8 8-bit -> bits_out expansion after eq. */
 enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
 
@@ -204,7 +214,8 @@ typedef struct h2s_params {
                           * npl                                            */
   int32_t chroma_edge;   /* enum h2s_chroma_edge (S1)                       */
   int32_t lut_input;     /* enum h2s_lut_input (S3 -> S4, CPU chain)        */
-  int32_t reserved[2];
+  int32_t lp_tone;       /* enum h2s_lp_tone (libplacebo branch)            */
+  int32_t reserved[1];
 } h2s_params;
 
 /* A batch of planar 4:2:0 frames (yuv420p / yuv420p10le / yuv420p12le).

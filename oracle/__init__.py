@@ -50,7 +50,7 @@ class Params(ctypes.Structure):
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
         ('lut_input', ctypes.c_int32),
-        ('reserved', ctypes.c_int32 * 2),
+        ('lp_tone', ctypes.c_int32), ('reserved', ctypes.c_int32 * 1),
     ]
 
 

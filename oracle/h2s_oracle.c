@@ -86,6 +86,8 @@ typedef struct {
   double min_lum, bp, bgain; /* BT.2390 black-point adaptation (PQ, source-normalised) */
   double out_scale;     /* curve output (PQ-normalised linear) -> units of tw */
   double enc_a, enc_b;  /* libplacebo BT.1886 encode: (x / a)^(1/2.4) - b   */
+  int ipt;              /* libplacebo branch: curve on IPT-PQ intensity      */
+  float r2l[3][3], l2r[3][3], i2l[3][3]; /* BT.2020 RGB -> LMS, inverse; IPT -> L'M'S' */
   int dither;           /* 1: ordered dither at the swscale 8-bit quantiser */
 } ocfg;
 
@@ -158,8 +160,7 @@ static float pq_encode_f(float y) {
  * black-point adaptation x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum
  * for a target black above 0, back to PQ over the source range.  Restated
  * from the published algorithm; libplacebo is absent: PARITY UNPINNED. */
-static float bt2390_sig(const ocfg *c, float sig) {
-  float e1 = pq_encode_f(sig * (float)(c->p->npl / 10000.0));
+static float bt2390_pq(const ocfg *c, float e1) {
   float e1n = (e1 - (float)c->src_min) / (float)(c->src_max - c->src_min);
   /* E1 is clipped to the source range; a NaN from an overflowed (inf) input
    * counts as above the range */
@@ -177,9 +178,12 @@ static float bt2390_sig(const ocfg *c, float sig) {
     e2 += mn * powf(1.0f - e2, (float)c->bp);
     e2 = (float)c->bgain * (e2 - mn) + mn;
   }
-  float e4 = e2 * (float)(c->src_max - c->src_min) + (float)c->src_min;
+  return e2 * (float)(c->src_max - c->src_min) + (float)c->src_min;
+}
+
+static float bt2390_sig(const ocfg *c, float sig) {
   /* back to linear, in units of the target white */
-  return st2084_eotf(e4) * (float)c->out_scale;
+  return st2084_eotf(bt2390_pq(c, pq_encode_f(sig * (float)(c->p->npl / 10000.0)))) * (float)c->out_scale;
 }
 
 /* libplacebo src/tone_mapping.c "spline" (scaling PL_HDR_PQ), restated from
@@ -250,10 +254,39 @@ static float spline_sig(const ocfg *c, float sig) {
 
 #define MIX(x, y, a) (x) * (1 - (a)) + (y) * (a)
 
+/* libplacebo branch, h2s_params.lp_tone = IPT: the PQ-domain curve on the
+ * intensity of IPT-PQ, P and T kept.  Linear BT.2020 R'G'B' (npl units) ->
+ * LMS (HPE of XYZ, D65-normalised so that neutral colours have L = M = S =
+ * Y) in absolute luminance / 10000 -> PQ -> I = 0.4 L' + 0.4 M' + 0.2 S',
+ * P, T (Ebner-Fairchild); I' = curve(I); back through the inverses, linear
+ * in units of the target white.  Neutral colours reduce to the MAX_RGB form
+ * (I = PQ(Y)).  Inputs are capped at 1e6 npl (the exact EOTF overflows to
+ * inf beyond E = 2, and inf - inf in the LMS rows would be NaN).  PARITY
+ * UNPINNED: libplacebo is absent. */
+static rgbf tone_ipt(const ocfg *c, rgbf in) {
+  const float s = (float)(c->p->npl / 10000.0);
+  const float v[3] = {fminf(in.r, 1e6f) * s, fminf(in.g, 1e6f) * s, fminf(in.b, 1e6f) * s};
+  float q[3];
+  for (int k = 0; k < 3; k++)
+    q[k] = pq_encode_f(c->r2l[k][0] * v[0] + c->r2l[k][1] * v[1] + c->r2l[k][2] * v[2]);
+  const float I = 0.4f * q[0] + 0.4f * q[1] + 0.2f * q[2];
+  const float P = 4.455f * q[0] - 4.851f * q[1] + 0.396f * q[2];
+  const float T = 0.8056f * q[0] + 0.3572f * q[1] - 1.1628f * q[2];
+  const float I2 = c->p->tonemap == H2S_TM_SPLINE ? spline_pq_f(c, I) : bt2390_pq(c, I);
+  float l[3];
+  for (int k = 0; k < 3; k++) l[k] = st2084_eotf(I2 + c->i2l[k][1] * P + c->i2l[k][2] * T);
+  const float os = (float)c->out_scale;
+  rgbf o = {(c->l2r[0][0] * l[0] + c->l2r[0][1] * l[1] + c->l2r[0][2] * l[2]) * os,
+            (c->l2r[1][0] * l[0] + c->l2r[1][1] * l[1] + c->l2r[1][2] * l[2]) * os,
+            (c->l2r[2][0] * l[0] + c->l2r[2][1] * l[1] + c->l2r[2][2] * l[2]) * os};
+  return o;
+}
+
 static rgbf tonemap_px(const ocfg *c, rgbf in) {
   rgbf o = in;
   float sig, sig_orig;
   int tm = c->p->tonemap;
+  if (c->ipt && (tm == H2S_TM_SPLINE || tm == H2S_TM_BT2390)) return tone_ipt(c, in);
   if (tm == H2S_TM_SPLINE) {
     sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
     float s2 = spline_sig(c, sig);
@@ -520,6 +553,44 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf 
 }
 
 /* ---- configuration ------------------------------------------------------ */
+/* IPT-PQ matrices for h2s_params.lp_tone = IPT, in double, rounded to float:
+ * BT.2020 RGB -> XYZ from the primaries and D65, XYZ -> LMS by the
+ * Hunt-Pointer-Estevez matrix IPT uses, their inverse, and the inverse of
+ * the Ebner-Fairchild L'M'S' -> IPT matrix (its first column is 1). */
+static void inv3(const double m[3][3], double o[3][3]) {
+  const double d = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                   m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      const int a = (j + 1) % 3, b = (j + 2) % 3, e = (i + 1) % 3, f = (i + 2) % 3;
+      o[i][j] = (m[a][e] * m[b][f] - m[a][f] * m[b][e]) / d;
+    }
+}
+
+static void ipt_matrices(float r2l[3][3], float l2r[3][3], float i2l[3][3]) {
+  const double xy[4][2] = {{0.708, 0.292}, {0.170, 0.797}, {0.131, 0.046}, {0.3127, 0.3290}};
+  double P[3][3], Pi[3][3], S[3], M[3][3];
+  for (int k = 0; k < 3; k++) {
+    P[0][k] = xy[k][0] / xy[k][1];
+    P[1][k] = 1.0;
+    P[2][k] = (1.0 - xy[k][0] - xy[k][1]) / xy[k][1];
+  }
+  inv3(P, Pi);
+  const double W[3] = {xy[3][0] / xy[3][1], 1.0, (1.0 - xy[3][0] - xy[3][1]) / xy[3][1]};
+  for (int i = 0; i < 3; i++) S[i] = Pi[i][0] * W[0] + Pi[i][1] * W[1] + Pi[i][2] * W[2];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) M[i][k] = P[i][k] * S[k];          /* RGB -> XYZ */
+  const double hpe[3][3] = {{0.4002, 0.7076, -0.0808}, {-0.2263, 1.1653, 0.0457}, {0.0, 0.0, 0.9182}};
+  const double ipt[3][3] = {{0.4, 0.4, 0.2}, {4.455, -4.851, 0.396}, {0.8056, 0.3572, -1.1628}};
+  double R[3][3], Ri[3][3], Ii[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) R[i][k] = hpe[i][0] * M[0][k] + hpe[i][1] * M[1][k] + hpe[i][2] * M[2][k];
+  inv3(R, Ri);
+  inv3(ipt, Ii);
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) r2l[i][k] = (float)R[i][k], l2r[i][k] = (float)Ri[i][k], i2l[i][k] = (float)Ii[i][k];
+}
+
 static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   memset(c, 0, sizeof(*c));
   c->p = p;
@@ -610,6 +681,8 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
     c->enc_a = pow(1.0 - lb, 2.4);
     c->enc_b = lb / (1.0 - lb);
   }
+  c->ipt = lp && p->lp_tone == H2S_LP_TONE_IPT;
+  ipt_matrices(c->r2l, c->l2r, c->i2l);
   /* BT.2390 constants (libplacebo bt2390): source [0, peak*100 nits] and
    * target [black, white] in PQ, normalised to the source range */
   c->src_min = pq_encode_d(0.0);
@@ -931,10 +1004,13 @@ int oracle_resolved(const h2s_params *p, double *peak, double *param, uint16_t *
   return c.q_bits;
 }
 
-/* single-pixel tone-curve probe: sig -> sig' (for known-answer tests) */
+/* single-pixel tone-curve probe: sig -> sig' (for known-answer tests); the
+ * curve itself, i.e. the MAX_RGB application on a neutral pixel (IPT's HPE
+ * normalisation would add its own 2e-5 rounding) */
 float oracle_tone_curve(const h2s_params *p, float sig) {
   ocfg c;
   resolve(&c, p, NULL, 0);
+  c.ipt = 0;
   h2s_params q = *p;
   q.desat = 0;
   c.p = &q;

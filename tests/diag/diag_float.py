@@ -5,7 +5,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(REPO, 'hdr-to-sdr_amd'), REPO]
 import oracle  # noqa: E402
 import hdr2sdr  # noqa: E402

@@ -1,11 +1,11 @@
 """Diagnostics for GPU-vs-oracle mismatches (prints distributions, worst
-entries).  Usage on the GPU box: python scripts/diag_parity.py"""
+entries).  Usage on the GPU box: python tests/diag/diag_parity.py"""
 import os
 import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(REPO, 'hdr-to-sdr_amd'), REPO, os.path.join(REPO, 'tests')]
 import oracle  # noqa: E402
 import hdr2sdr  # noqa: E402

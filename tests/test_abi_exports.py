@@ -46,6 +46,7 @@ def test_abi_version_and_defaults():
     assert p.tm_param != p.tm_param  # NaN = filter default
     # [EXT] switches default to the round-1 models; libplacebo targets NaN = branch default
     assert (p.chroma_filter, p.dither, p.expand, p.pipeline, p.chroma_edge, p.lut_input) == (0, 0, 0, 0, 0, 0)
+    assert p.lp_tone == _abi.LP_TONE_IPT
     for v in (p.knee_offset, p.target_black, p.target_white):
         assert v != v
 
@@ -55,11 +56,11 @@ PROBE = r'''
 #include <stdio.h>
 #include "h2s.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(h2s_params), offsetof(h2s_params, tm_param),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(h2s_params), offsetof(h2s_params, tm_param),
          offsetof(h2s_params, lut_enabled), offsetof(h2s_params, desat_luma), sizeof(h2s_frames),
          offsetof(h2s_frames, width), offsetof(h2s_params, pipeline), offsetof(h2s_params, knee_offset),
          offsetof(h2s_params, target_white), offsetof(h2s_params, chroma_edge),
-         offsetof(h2s_params, lut_input));
+         offsetof(h2s_params, lut_input), offsetof(h2s_params, lp_tone));
   return 0;
 }
 '''
@@ -74,7 +75,7 @@ def test_struct_layout_matches_c(tmp_path):
     for P, F in ((_abi.H2SParams, _abi.H2SFrames), (oracle.Params, oracle.Frames)):
         want = [ctypes.sizeof(P), P.tm_param.offset, P.lut_enabled.offset, P.desat_luma.offset,
                 ctypes.sizeof(F), F.width.offset, P.pipeline.offset, P.knee_offset.offset,
-                P.target_white.offset, P.chroma_edge.offset, P.lut_input.offset]
+                P.target_white.offset, P.chroma_edge.offset, P.lut_input.offset, P.lp_tone.offset]
         assert got == want
 
 

@@ -216,7 +216,9 @@ FLOAT_CFGS = {
     'C4_mobius_native': dict(tonemapper='mobius', bits_out=10, mode='native'),
     # the libplacebo branch (the reference's C3 chain, src/utils.py:444-460):
     # knee offset 1.0, black point 0.203 nits, target white 203, rgba8 + lut3d 8-bit
+    # (tone curve on the IPT-PQ intensity, the default; and the max(R,G,B) gain)
     'C3_bt2390_libplacebo': dict(tonemapper='bt.2390', bits_out=10),
+    'C3_bt2390_libplacebo_max_rgb': dict(tonemapper='bt.2390', bits_out=10, lp_tone='max-rgb'),
     'spline_libplacebo_hlg12': dict(tonemapper='spline', bits_in=12, bits_out=12, transfer='arib-std-b67'),
 }
 

@@ -103,6 +103,10 @@ LP_CASES = {
     'bt2390_8bit': dict(tonemapper='bt.2390', bits_out=8),
     'bt2390_hlg12': dict(tonemapper='bt.2390', bits_in=12, bits_out=12, transfer='arib-std-b67'),
     'bt2390_lut_off_nv12': dict(tonemapper='bt.2390', lut_enabled=False),
+    'bt2390_max_rgb': dict(tonemapper='bt.2390', lp_tone='max-rgb'),
+    'spline_max_rgb_hlg12': dict(tonemapper='spline', lp_tone='max-rgb', bits_in=12, bits_out=12,
+                                 transfer='arib-std-b67'),
+    'bt2390_max_rgb_lut_off': dict(tonemapper='bt.2390', lp_tone='max-rgb', lut_enabled=False),
 }
 
 
@@ -117,7 +121,7 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
     assert _path(tm, params, 128, 64) == (_abi.PATH_TILE if params.lut_enabled else _abi.PATH_GENERIC)
 
 
-@pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12'])
+@pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb'])
 def test_libplacebo_tile_equals_generic(tm, case):
     """The two kernels of the libplacebo branch against each other (same
     device, same float32 formulas up to the tile kernel's PQ table): the
@@ -134,6 +138,27 @@ def test_libplacebo_tile_equals_generic(tm, case):
         tm.set_option(_abi.OPT_FAST_PATH, 1)
     assert_close_int(params, tile, gen, 256, 64)
     assert (tile == gen).mean() > 0.99
+
+
+def test_lp_tone_ipt_changes_only_coloured_pixels(tm):
+    """h2s_lp_tone: IPT and MAX_RGB apply the same curve, so neutral pixels
+    (R = G = B) agree within the HPE normalisation's rounding; coloured ones
+    differ."""
+    W, H = 128, 64
+    src = hdr2sdr.FrameBatch.empty_numpy(1, W, H, 10)
+    src.y[0] = np.linspace(64, 940, W * H).reshape(H, W).astype(np.uint16)
+    src.u[0] = 512
+    src.v[0] = 512
+    ipt = hdr2sdr.TonemapParams(tonemapper='bt.2390')
+    outs = []
+    for p in (ipt, ipt.with_(lp_tone='max-rgb')):
+        tm.set_params(p)
+        tm.set_lut(lattice(65))
+        outs.append(tm(src.to_torch('cuda')).to_numpy().buf.astype(np.int64))
+    assert np.abs(outs[0] - outs[1]).max() <= 2 and (outs[0] != outs[1]).mean() < 0.01
+    col, _, _ = run_both(tm, ipt, 'smooth', W, H)
+    col2, _, _ = run_both(tm, ipt.with_(lp_tone='max-rgb'), 'smooth', W, H)
+    assert (col != col2).mean() > 0.05
 
 
 def test_libplacebo_rgba_codes_use_the_full_output_depth(tm):
