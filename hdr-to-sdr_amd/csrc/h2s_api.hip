@@ -53,6 +53,7 @@ struct h2s_ctx {
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
+  float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
   void* d_prev = nullptr;  // preview scratch
@@ -234,11 +235,10 @@ double pq_eotf_d(double e) {
   return pow(num / (c2 - c3 * xp), 1.0 / m1);
 }
 
-// IPT-PQ matrices (h2s_lp_tone IPT), built in double and rounded once:
-// BT.2020 RGB -> XYZ from the primaries and D65 white, XYZ -> LMS by the
-// Hunt-Pointer-Estevez matrix of IPT (D65-normalised: neutral L = M = S = Y),
-// the inverse, and the inverse of the Ebner-Fairchild L'M'S' -> IPT matrix
-// (its I column is exactly 1: the P and T rows sum to 0)
+// IPT-PQ matrices (h2s_lp_tone IPT), in double: BT.2020 RGB -> XYZ from the
+// primaries and D65 white, XYZ -> LMS by the Hunt-Pointer-Estevez matrix of
+// IPT (D65-normalised: neutral L = M = S = Y), and the inverse.  Keeping P and
+// T reduces to L'M'S' += I' - I (the inverse IPT matrix has an I column of 1)
 static void inv3(const double m[3][3], double o[3][3]) {
   const double d = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
                    m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
@@ -248,7 +248,7 @@ static void inv3(const double m[3][3], double o[3][3]) {
                  m[(j + 1) % 3][(i + 2) % 3] * m[(j + 2) % 3][(i + 1) % 3]) / d;
 }
 
-static void ipt_matrices(float r2l[9], float l2r[9], float i2l[9]) {
+static void ipt_matrices(double r2l[9], double l2r[9]) {
   const double prim[3][2] = {{0.708, 0.292}, {0.170, 0.797}, {0.131, 0.046}}, wx = 0.3127, wy = 0.3290;
   double xyz[3][3], xyzi[3][3];
   for (int k = 0; k < 3; k++) {
@@ -263,13 +263,11 @@ static void ipt_matrices(float r2l[9], float l2r[9], float i2l[9]) {
     for (int i = 0; i < 3; i++) xyz[i][k] *= sk;                       // RGB -> XYZ
   }
   const double hpe[3][3] = {{0.4002, 0.7076, -0.0808}, {-0.2263, 1.1653, 0.0457}, {0.0, 0.0, 0.9182}};
-  const double ipt[3][3] = {{0.4, 0.4, 0.2}, {4.455, -4.851, 0.396}, {0.8056, 0.3572, -1.1628}};
-  double rl[3][3], lr[3][3], il[3][3];
+  double rl[3][3], lr[3][3];
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++) rl[i][k] = hpe[i][0] * xyz[0][k] + hpe[i][1] * xyz[1][k] + hpe[i][2] * xyz[2][k];
   inv3(rl, lr);
-  inv3(ipt, il);
-  for (int i = 0; i < 9; i++) r2l[i] = (float)rl[i / 3][i % 3], l2r[i] = (float)lr[i / 3][i % 3], i2l[i] = (float)il[i / 3][i % 3];
+  for (int i = 0; i < 9; i++) r2l[i] = rl[i / 3][i % 3], l2r[i] = lr[i / 3][i % 3];
 }
 
 void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
@@ -343,7 +341,7 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   const bool lp = k->pipe == h2s::PIPE_LIBPLACEBO;
   k->rgba8 = lp && p->lut_enabled ? 1 : 0;
   k->lp_ipt = lp && p->lp_tone == H2S_LP_TONE_IPT ? 1 : 0;
-  ipt_matrices(k->ipt_r2l, k->ipt_l2r, k->ipt_i2l);
+  ipt_matrices(k->ipt_r2l, k->ipt_l2r);
   k->t_white = isnan(p->target_white) ? (lp ? 203.0 : p->npl) : p->target_white;
   k->t_black = isnan(p->target_black) ? (lp ? k->t_white / 1000.0 : 0.0) : p->target_black;
   k->knee_off = isnan(p->knee_offset) ? 1.0 : p->knee_offset;
@@ -357,6 +355,7 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   spline_consts(peak, 0.0, k->sp_contrast, k);
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / k->t_white);
+  k->ipt_npl = p->npl / 10000.0, k->ipt_os = 10000.0 / k->t_white;
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
   const double m[9] = {1.6604910021, -0.5876411388, -0.0728498633, -0.1245504745, 1.1328998971,
                        -0.0083494226, -0.0181507634, -0.1005788980, 1.1187296614};
@@ -395,6 +394,46 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
     if (o != i) ident = false;
   }
   k->eq_identity = ident ? 1 : 0;
+}
+
+// ST 2084 inverse EOTF (y = luminance / 10000 -> E) as PQI_NSEG cubic
+// segments for the tile kernel's IPT form (h2s_tile.h pqi): segment s covers
+// y = 2^e (1 + j/4 + t), e = PQI_OCT0 + s/4, j = s%4, t in [0, 1/4), read from
+// the float's exponent and top two mantissa bits; the cubic in t through the
+// exact (double) encode at the 4 Chebyshev nodes.  Max relative error 1.1e-6
+// (near y = 2^-15) with float32 coefficients; below 2^-40 (1e-8 nits) the
+// first segment is used (E < 1.5e-5)
+static void solve_cubic(const double t[4], const double y[4], double c[4]) {
+  double A[4][5];
+  for (int k = 0; k < 4; k++) {
+    for (int j = 0; j < 4; j++) A[k][j] = pow(t[k], j);
+    A[k][4] = y[k];
+  }
+  for (int col = 0; col < 4; col++) {
+    int piv = col;
+    for (int r = col + 1; r < 4; r++)
+      if (fabs(A[r][col]) > fabs(A[piv][col])) piv = r;
+    for (int j = 0; j < 5; j++) std::swap(A[col][j], A[piv][j]);
+    for (int r = 0; r < 4; r++) {
+      if (r == col) continue;
+      const double fct = A[r][col] / A[col][col];
+      for (int j = col; j < 5; j++) A[r][j] -= fct * A[col][j];
+    }
+  }
+  for (int k = 0; k < 4; k++) c[k] = A[k][4] / A[k][k];
+}
+
+void build_pqi_table(std::vector<float4>* out) {
+  out->resize(h2s::PQI_NSEG);
+  double t[4];
+  for (int k = 0; k < 4; k++) t[k] = (1.0 - cos((2 * k + 1) * M_PI / 8.0)) / 2.0 * 0.25;
+  for (int sg = 0; sg < h2s::PQI_NSEG; sg++) {
+    const double base = ldexp(1.0, h2s::PQI_OCT0 + sg / 4);
+    double y[4], c[4];
+    for (int k = 0; k < 4; k++) y[k] = pq_encode_d(base * (1.0 + (sg % 4) * 0.25 + t[k]));
+    solve_cubic(t, y, c);
+    (*out)[sg] = make_float4((float)c[3], (float)c[2], (float)c[1], (float)c[0]);
+  }
 }
 
 // PQ EOTF x scale as PQ_NSEG cubic segments: per segment, the cubic through
@@ -614,6 +653,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_lut_yuv) hipFree(c->d_lut_yuv);
   if (c->d_eq) hipFree(c->d_eq);
   if (c->d_pq) hipFree(c->d_pq);
+  if (c->d_pqi) hipFree(c->d_pqi);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
   if (c->d_peak) hipFree(c->d_peak);
@@ -690,13 +730,25 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   if (e != hipSuccess) return hip_fail(c, e, "eq table upload");
   {
     std::vector<float4> pq;
-    build_pq_table((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl, &pq);
+    // (x 10000/npl for either input transfer: the libplacebo branch's IPT form
+    // decodes PQ L'M'S' through it for HLG input too)
+    build_pq_table(10000.0 / p->npl, &pq);
     if (!c->d_pq && (e = hipMalloc((void**)&c->d_pq, pq.size() * sizeof(float4))) != hipSuccess) {
       c->d_pq = nullptr;
       return fail(c, H2S_E_OOM, "PQ table allocation failed");
     }
     if ((e = hipMemcpy(c->d_pq, pq.data(), pq.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
       return hip_fail(c, e, "PQ table upload");
+    if (!c->d_pqi) {
+      std::vector<float4> pqi;
+      build_pqi_table(&pqi);
+      if ((e = hipMalloc((void**)&c->d_pqi, pqi.size() * sizeof(float4))) != hipSuccess) {
+        c->d_pqi = nullptr;
+        return fail(c, H2S_E_OOM, "PQ encode table allocation failed");
+      }
+      if ((e = hipMemcpy(c->d_pqi, pqi.data(), pqi.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(c, e, "PQ encode table upload");
+    }
   }
   c->params = *p;
   c->k = k;
@@ -779,8 +831,9 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->c56 = 56.0f * k.qscale;
   for (int i = 0; i < 3; i++) F->k709[i] = k.k709[i], F->kcb[i] = k.kcb[i], F->kcr[i] = k.kcr[i];
   F->lp_ipt = k.lp_ipt;
-  for (int i = 0; i < 9; i++) F->ipt_r2l[i] = (float)((double)k.ipt_r2l[i] * (double)k.npl_1e4), F->ipt_l2r[i] = k.ipt_l2r[i];
-  for (int i = 0; i < 3; i++) F->ipt_pt[2 * i] = k.ipt_i2l[3 * i + 1], F->ipt_pt[2 * i + 1] = k.ipt_i2l[3 * i + 2];
+  for (int i = 0; i < 9; i++)
+    F->ipt_r2l[i] = (float)(k.ipt_r2l[i] * k.ipt_npl), F->ipt_l2r[i] = (float)(k.ipt_l2r[i] * (p->npl / k.t_white));
+  F->pqi_tab = c->d_pqi;
   curve_fast(k, F);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));

@@ -49,7 +49,8 @@ struct KParams {
   int pipe, rgba8;
   float enc_ainv, enc_b;  // libplacebo BT.1886 encode: (x * ainv)^(1/2.4) - b
   int lp_ipt;             // libplacebo branch: the curve on IPT-PQ intensity (h2s_lp_tone IPT)
-  float ipt_r2l[9], ipt_l2r[9], ipt_i2l[9];  // BT.2020 RGB -> LMS, inverse; IPT -> L'M'S' (row-major)
+  double ipt_r2l[9], ipt_l2r[9];  // BT.2020 RGB -> LMS (HPE), inverse (row-major)
+  double ipt_npl, ipt_os;         // npl / 10000, 10000 / target white (double)
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
   float lut_max;
@@ -131,9 +132,10 @@ struct FastParams : CurveConsts {
   float lp_k1, lp_k2, lp_xmax, nm1, inv255, qscale, c56;
   float k709[3], kcb[3], kcr[3];
   // lp_tone = IPT: RGB (npl units) -> LMS / 10000 (npl/10000 folded in); LMS
-  // -> RGB; the P and T columns of IPT -> L'M'S' (the I column is 1)
+  // -> RGB; the PQ encode as PQI_NSEG cubic segments (pqi)
   int lp_ipt;
-  float ipt_r2l[9], ipt_l2r[9], ipt_pt[6];
+  float ipt_r2l[9], ipt_l2r[9];
+  const float4* pqi_tab;
   const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
@@ -161,6 +163,8 @@ struct FastParams : CurveConsts {
 constexpr int PQ_SEG = 128;          // segments per unit of E
 constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
 constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
+constexpr int PQI_OCT0 = -40;        // PQ encode table: first octave 2^-40 (x 10000 nits)
+constexpr int PQI_NSEG = 54 * 4;     // octaves 2^-40 .. 2^14, four segments each
 
 struct YuvLutConsts {
   float s, k709[3], kcb[3], kcr[3];
@@ -253,25 +257,33 @@ __device__ __forceinline__ float bt2390_pq(const KParams& P, float e1) {
 }
 
 // libplacebo branch, h2s_lp_tone IPT (oracle tone_ipt): the PQ-domain curve
-// on the intensity of IPT-PQ, P and T kept; linear in, linear out (units of
-// npl in, of the target white out)
+// on the intensity of IPT-PQ, P and T kept, i.e. L'M'S' += I' - I.  In double
+// around the float curve, as the oracle: the LMS -> RGB rows turn float32
+// EOTF noise into large errors on channels they cancel to near zero
+__device__ __forceinline__ double pq_encode_dd(double y) {
+  const double ym = pow(fmax(y, 0.0), (double)PQ_M1);
+  return pow(((double)PQ_C1 + (double)PQ_C2 * ym) / (1.0 + (double)PQ_C3 * ym), (double)PQ_M2);
+}
+__device__ __forceinline__ double pq_eotf_dd(double e) {
+  if (!(e > 0.0)) return 0.0;
+  const double xp = pow(e, 1.0 / (double)PQ_M2);
+  return pow(fmax(xp - (double)PQ_C1, 0.0) / ((double)PQ_C2 - (double)PQ_C3 * xp), 1.0 / (double)PQ_M1);
+}
 __device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, float& b) {
-  const float s = P.npl_1e4;
-  const float v0 = fminf(r, 1e6f) * s, v1 = fminf(g, 1e6f) * s, v2 = fminf(b, 1e6f) * s;
-  float q[3];
+  const double s = P.ipt_npl;
+  const double v0 = fmin((double)r, 1e6) * s, v1 = fmin((double)g, 1e6) * s, v2 = fmin((double)b, 1e6) * s;
+  double q[3];
 #pragma unroll
-  for (int k = 0; k < 3; k++) q[k] = pq_encode(P.ipt_r2l[3 * k] * v0 + P.ipt_r2l[3 * k + 1] * v1 + P.ipt_r2l[3 * k + 2] * v2);
-  const float I = 0.4f * q[0] + 0.4f * q[1] + 0.2f * q[2];
-  const float Pc = 4.455f * q[0] - 4.851f * q[1] + 0.396f * q[2];
-  const float T = 0.8056f * q[0] + 0.3572f * q[1] - 1.1628f * q[2];
-  const float I2 = P.tonemap == 8 ? spline_pq(P, I) : bt2390_pq(P, I);
-  float l[3];
+  for (int k = 0; k < 3; k++) q[k] = pq_encode_dd(P.ipt_r2l[3 * k] * v0 + P.ipt_r2l[3 * k + 1] * v1 + P.ipt_r2l[3 * k + 2] * v2);
+  const double I = 0.4 * q[0] + 0.4 * q[1] + 0.2 * q[2];
+  const double dI = (double)(P.tonemap == 8 ? spline_pq(P, (float)I) : bt2390_pq(P, (float)I)) - I;
+  double l[3];
 #pragma unroll
-  for (int k = 0; k < 3; k++) l[k] = pq_eotf(I2 + P.ipt_i2l[3 * k + 1] * Pc + P.ipt_i2l[3 * k + 2] * T);
-  const float os = P.e4_npl;
-  r = (P.ipt_l2r[0] * l[0] + P.ipt_l2r[1] * l[1] + P.ipt_l2r[2] * l[2]) * os;
-  g = (P.ipt_l2r[3] * l[0] + P.ipt_l2r[4] * l[1] + P.ipt_l2r[5] * l[2]) * os;
-  b = (P.ipt_l2r[6] * l[0] + P.ipt_l2r[7] * l[1] + P.ipt_l2r[8] * l[2]) * os;
+  for (int k = 0; k < 3; k++) l[k] = pq_eotf_dd(q[k] + dI);
+  const double os = P.ipt_os;
+  r = (float)((P.ipt_l2r[0] * l[0] + P.ipt_l2r[1] * l[1] + P.ipt_l2r[2] * l[2]) * os);
+  g = (float)((P.ipt_l2r[3] * l[0] + P.ipt_l2r[4] * l[1] + P.ipt_l2r[5] * l[2]) * os);
+  b = (float)((P.ipt_l2r[6] * l[0] + P.ipt_l2r[7] * l[1] + P.ipt_l2r[8] * l[2]) * os);
 }
 
 // S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)

@@ -82,6 +82,18 @@ __device__ __forceinline__ float pq_z(const float4* tab, float u) {
 // staged E (table-segment units, +1) at and above which pq_z is invalid
 constexpr float PQZ_LIM = PQ_EMAX * (float)PQ_SEG + 1.0f;
 
+// ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
+// (build_pqi_table): the segment is the float's exponent and top two mantissa
+// bits, t the remaining 21 mantissa bits as [0, 1/4); clamped to the table's
+// octaves 2^-40 .. 2^14
+__device__ __forceinline__ float pqi(const float4* tab, float y) {
+  const unsigned b = __builtin_bit_cast(unsigned, y) & 0x7FFFFFFFu;
+  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG - 1);
+  const float t = __builtin_bit_cast(float, (b & 0x1FFFFFu) | 0x3F800000u) - 1.0f;
+  const float4 c = tab[sg];
+  return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
+}
+
 // S1 transfer to linear (units of npl), specialised
 // returns true (wave-uniform) when some lane of the wave took the exact PQ
 // path: linear values may then be huge or infinite, and the tone curve must
@@ -134,11 +146,12 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // input's own max code value (emax_s = max E * PQ_SEG + 1, clamped below at
 // the code of sig = 1e-6); the final decode reads the EOTF table in LDS.
 // libplacebo branch with h2s_lp_tone IPT (F.lp_ipt): the curve acts on the
-// intensity of IPT-PQ instead (three exact PQ encodes of the LMS rows, three
-// table decodes of L'M'S' = I' + a P + b T), as the oracle's tone_ipt.
+// intensity of IPT-PQ instead (three LMS rows encoded through the PQ-encode
+// table, L'M'S' += I' - I decoded through the EOTF table), as the oracle's
+// tone_ipt.
 template <int TRC, int TM, int DESAT>
-__device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds, float& r,
-                                     float& g, float& b, bool safe, float emax_s) {
+__device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
+                                     const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s) {
   if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
     // PQ input: the curve straight into pq_z's table coordinate u = e4*PQ_SEG
     // + 1 (the output scale and offset are folded into the polynomial
@@ -193,34 +206,22 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
     };
     if (F.lp_ipt) {
       // libplacebo branch, h2s_lp_tone IPT (oracle tone_ipt): the curve on
-      // the intensity of IPT-PQ, P and T kept (launch-uniform branch)
+      // the intensity of IPT-PQ with P and T kept, i.e. L'M'S' += I' - I;
+      // encode and decode through the LDS tables (launch-uniform branch; the
+      // EOTF table is staged for HLG input too)
       const float R = fminf(r, 1e6f), G = fminf(g, 1e6f), B = fminf(b, 1e6f);
-      const float q0 = pq_enc(F.ipt_r2l[0] * R + F.ipt_r2l[1] * G + F.ipt_r2l[2] * B);
-      const float q1 = pq_enc(F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
-      const float q2 = pq_enc(F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
+      const float q0 = pqi(pqi_lds, F.ipt_r2l[0] * R + F.ipt_r2l[1] * G + F.ipt_r2l[2] * B);
+      const float q1 = pqi(pqi_lds, F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
+      const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
       const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
-      const float Pc = 4.455f * q0 - 4.851f * q1 + 0.396f * q2;
-      const float T = 0.8056f * q0 + 0.3572f * q1 - 1.1628f * q2;
-      float l0, l1, l2, os;
-      if (TRC == 0) {   // L' = I' + a P + b T on the EOTF table's coordinate
-        const float u = curve_u(I);
-        const float ps = Pc * (float)PQ_SEG, ts = T * (float)PQ_SEG;
-        auto lz = [&](int k) {
-          return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(F.ipt_pt[2 * k], ps, fmaf(F.ipt_pt[2 * k + 1], ts, u)), 1.0f,
-                                                      PQZ_LIM - 0.01f));
-        };
-        l0 = lz(0), l1 = lz(1), l2 = lz(2);
-        os = F.tw_fold;
-      } else {
-        const float e4 = curve_e4(I);
-        l0 = eotf_exact(e4 + F.ipt_pt[0] * Pc + F.ipt_pt[1] * T);
-        l1 = eotf_exact(e4 + F.ipt_pt[2] * Pc + F.ipt_pt[3] * T);
-        l2 = eotf_exact(e4 + F.ipt_pt[4] * Pc + F.ipt_pt[5] * T);
-        os = F.e4_npl;
-      }
-      r = (F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2) * os;
-      g = (F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2) * os;
-      b = (F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2) * os;
+      const float du = curve_u(I) - I * (float)PQ_SEG;   // (I' - I) PQ_SEG + 1
+      auto lz = [&](float q) {
+        return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f));
+      };
+      const float l0 = lz(q0), l1 = lz(q1), l2 = lz(q2);
+      r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
+      g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
+      b = F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2;
       return;
     }
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
@@ -420,7 +421,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
-  __shared__ float4 pq_lds[TRC == 0 ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
+  __shared__ float4 pq_lds[(TRC == 0 || LP) ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
+  __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
@@ -437,15 +439,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
   const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * t, 0, 0);  // out of range -> 0
   float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (TRC == 0 && t < PQ_NSEG) {
+  const bool stage_pq = TRC == 0 || (LP && F.lp_ipt);   // block-uniform
+  if (stage_pq && t < PQ_NSEG) {
     const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
     pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
   }
   if (t < F.eq_n) eq_lds[t] = (uint16_t)(eq0 << F.shift_out);
   for (int i = t + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
     eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
-  if (TRC == 0 && t < PQ_NSEG) pq_lds[t + 1] = pq0;
-  if (TRC == 0 && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
+  if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (LP && F.lp_ipt) {
+    const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
+    for (int i = t; i < PQI_NSEG; i += 256)
+      pqi_lds[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpi, 16 * i, 0, 0));
+  }
 
   // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block
   // (2w + (s&1), s>>1); lane = pixel (quad q = lane>>2 in a 4x4 quad grid,
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
       };
       if (DBG == 1) dput(r, gg, bl);
-      tone<TRC, TM, DESAT>(F, cv, pq_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
+      tone<TRC, TM, DESAT>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
       if (DBG == 2) dput(r, gg, bl);
       float sr, sg, sb;
       if (LP) {

@@ -87,7 +87,7 @@ typedef struct {
   double out_scale;     /* curve output (PQ-normalised linear) -> units of tw */
   double enc_a, enc_b;  /* libplacebo BT.1886 encode: (x / a)^(1/2.4) - b   */
   int ipt;              /* libplacebo branch: curve on IPT-PQ intensity      */
-  float r2l[3][3], l2r[3][3], i2l[3][3]; /* BT.2020 RGB -> LMS, inverse; IPT -> L'M'S' */
+  double r2l[3][3], l2r[3][3]; /* BT.2020 RGB -> LMS (HPE), inverse           */
   int dither;           /* 1: ordered dither at the swscale 8-bit quantiser */
 } ocfg;
 
@@ -256,29 +256,31 @@ static float spline_sig(const ocfg *c, float sig) {
 
 /* libplacebo branch, h2s_params.lp_tone = IPT: the PQ-domain curve on the
  * intensity of IPT-PQ, P and T kept.  Linear BT.2020 R'G'B' (npl units) ->
- * LMS (HPE of XYZ, D65-normalised so that neutral colours have L = M = S =
- * Y) in absolute luminance / 10000 -> PQ -> I = 0.4 L' + 0.4 M' + 0.2 S',
- * P, T (Ebner-Fairchild); I' = curve(I); back through the inverses, linear
+ * LMS (HPE of XYZ, D65-normalised so that a neutral has L = M = S = Y) in
+ * absolute luminance / 10000 -> PQ -> I = 0.4 L' + 0.4 M' + 0.2 S' (the
+ * Ebner-Fairchild I row); I' = curve(I).  The inverse IPT matrix has an I
+ * column of ones, so keeping P and T means L'M'S' = (L', M', S') + (I' - I):
+ * no P/T round trip is needed.  Back through the EOTF and LMS -> RGB, linear
  * in units of the target white.  Neutral colours reduce to the MAX_RGB form
- * (I = PQ(Y)).  Inputs are capped at 1e6 npl (the exact EOTF overflows to
- * inf beyond E = 2, and inf - inf in the LMS rows would be NaN).  PARITY
- * UNPINNED: libplacebo is absent. */
+ * up to the HPE normalisation (2e-5).  Evaluated in double around the float
+ * curve: the LMS -> RGB rows (absolute sums up to 5.3) turn float32 EOTF
+ * noise (~4e-5) into visible errors on channels they cancel to near zero.
+ * Inputs are capped at 1e6 npl (the exact EOTF overflows to inf beyond E =
+ * 2).  PARITY UNPINNED: libplacebo is absent. */
 static rgbf tone_ipt(const ocfg *c, rgbf in) {
-  const float s = (float)(c->p->npl / 10000.0);
-  const float v[3] = {fminf(in.r, 1e6f) * s, fminf(in.g, 1e6f) * s, fminf(in.b, 1e6f) * s};
-  float q[3];
-  for (int k = 0; k < 3; k++)
-    q[k] = pq_encode_f(c->r2l[k][0] * v[0] + c->r2l[k][1] * v[1] + c->r2l[k][2] * v[2]);
-  const float I = 0.4f * q[0] + 0.4f * q[1] + 0.2f * q[2];
-  const float P = 4.455f * q[0] - 4.851f * q[1] + 0.396f * q[2];
-  const float T = 0.8056f * q[0] + 0.3572f * q[1] - 1.1628f * q[2];
-  const float I2 = c->p->tonemap == H2S_TM_SPLINE ? spline_pq_f(c, I) : bt2390_pq(c, I);
-  float l[3];
-  for (int k = 0; k < 3; k++) l[k] = st2084_eotf(I2 + c->i2l[k][1] * P + c->i2l[k][2] * T);
-  const float os = (float)c->out_scale;
-  rgbf o = {(c->l2r[0][0] * l[0] + c->l2r[0][1] * l[1] + c->l2r[0][2] * l[2]) * os,
-            (c->l2r[1][0] * l[0] + c->l2r[1][1] * l[1] + c->l2r[1][2] * l[2]) * os,
-            (c->l2r[2][0] * l[0] + c->l2r[2][1] * l[1] + c->l2r[2][2] * l[2]) * os};
+  const double s = c->p->npl / 10000.0;
+  const double v[3] = {fmin(in.r, 1e6) * s, fmin(in.g, 1e6) * s, fmin(in.b, 1e6) * s};
+  double q[3];
+  for (int k = 0; k < 3; k++) q[k] = pq_encode_d(c->r2l[k][0] * v[0] + c->r2l[k][1] * v[1] + c->r2l[k][2] * v[2]);
+  const double I = 0.4 * q[0] + 0.4 * q[1] + 0.2 * q[2];
+  const double dI =
+      (double)(c->p->tonemap == H2S_TM_SPLINE ? spline_pq_f(c, (float)I) : bt2390_pq(c, (float)I)) - I;
+  double l[3];
+  for (int k = 0; k < 3; k++) l[k] = pq_eotf_dd(q[k] + dI);
+  const double os = c->out_scale;
+  rgbf o = {(float)((c->l2r[0][0] * l[0] + c->l2r[0][1] * l[1] + c->l2r[0][2] * l[2]) * os),
+            (float)((c->l2r[1][0] * l[0] + c->l2r[1][1] * l[1] + c->l2r[1][2] * l[2]) * os),
+            (float)((c->l2r[2][0] * l[0] + c->l2r[2][1] * l[1] + c->l2r[2][2] * l[2]) * os)};
   return o;
 }
 
@@ -553,10 +555,9 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf 
 }
 
 /* ---- configuration ------------------------------------------------------ */
-/* IPT-PQ matrices for h2s_params.lp_tone = IPT, in double, rounded to float:
- * BT.2020 RGB -> XYZ from the primaries and D65, XYZ -> LMS by the
- * Hunt-Pointer-Estevez matrix IPT uses, their inverse, and the inverse of
- * the Ebner-Fairchild L'M'S' -> IPT matrix (its first column is 1). */
+/* IPT-PQ matrices for h2s_params.lp_tone = IPT, in double: BT.2020 RGB ->
+ * XYZ from the primaries and D65, XYZ -> LMS by the Hunt-Pointer-Estevez
+ * matrix IPT uses, and the inverse. */
 static void inv3(const double m[3][3], double o[3][3]) {
   const double d = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
                    m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
@@ -567,7 +568,7 @@ static void inv3(const double m[3][3], double o[3][3]) {
     }
 }
 
-static void ipt_matrices(float r2l[3][3], float l2r[3][3], float i2l[3][3]) {
+static void ipt_matrices(double r2l[3][3], double l2r[3][3]) {
   const double xy[4][2] = {{0.708, 0.292}, {0.170, 0.797}, {0.131, 0.046}, {0.3127, 0.3290}};
   double P[3][3], Pi[3][3], S[3], M[3][3];
   for (int k = 0; k < 3; k++) {
@@ -581,14 +582,9 @@ static void ipt_matrices(float r2l[3][3], float l2r[3][3], float i2l[3][3]) {
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++) M[i][k] = P[i][k] * S[k];          /* RGB -> XYZ */
   const double hpe[3][3] = {{0.4002, 0.7076, -0.0808}, {-0.2263, 1.1653, 0.0457}, {0.0, 0.0, 0.9182}};
-  const double ipt[3][3] = {{0.4, 0.4, 0.2}, {4.455, -4.851, 0.396}, {0.8056, 0.3572, -1.1628}};
-  double R[3][3], Ri[3][3], Ii[3][3];
   for (int i = 0; i < 3; i++)
-    for (int k = 0; k < 3; k++) R[i][k] = hpe[i][0] * M[0][k] + hpe[i][1] * M[1][k] + hpe[i][2] * M[2][k];
-  inv3(R, Ri);
-  inv3(ipt, Ii);
-  for (int i = 0; i < 3; i++)
-    for (int k = 0; k < 3; k++) r2l[i][k] = (float)R[i][k], l2r[i][k] = (float)Ri[i][k], i2l[i][k] = (float)Ii[i][k];
+    for (int k = 0; k < 3; k++) r2l[i][k] = hpe[i][0] * M[0][k] + hpe[i][1] * M[1][k] + hpe[i][2] * M[2][k];
+  inv3(r2l, l2r);
 }
 
 static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
@@ -682,7 +678,7 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
     c->enc_b = lb / (1.0 - lb);
   }
   c->ipt = lp && p->lp_tone == H2S_LP_TONE_IPT;
-  ipt_matrices(c->r2l, c->l2r, c->i2l);
+  ipt_matrices(c->r2l, c->l2r);
   /* BT.2390 constants (libplacebo bt2390): source [0, peak*100 nits] and
    * target [black, white] in PQ, normalised to the source range */
   c->src_min = pq_encode_d(0.0);

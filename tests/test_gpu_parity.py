@@ -209,6 +209,7 @@ def test_lut_sizes(tm, lut_n):
 #   stage 3/4 (gamma-encoded / post-LUT R'G'B'): 3.2e-4 at most in gamma space
 #     through x^(1/2.4) near black, and the LUT's slopes up to ~1.7: 6e-4;
 #   stage 5 (quantiser inputs, code units at depth q): 219 * 2^(q-8) * 3e-4.
+EPS_IPT = 1e-4     # LMS relative error of the IPT form on the tile kernel (tests/diag/diag_ipt.py: <= 5.6e-5)
 FLOAT_CFGS = {
     'C2_hable_pq10': dict(tonemapper='hable', gamma=2.2, bits_out=10),
     'C3_bt2390_pq10_cpu': dict(tonemapper='bt.2390', pipeline='cpu', bits_out=10),
@@ -296,6 +297,19 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
             gain = np.nanmax(np.abs(want), axis=0) / np.nanmax(np.abs(lin), axis=0)
         floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens
     tol = (1e-3 + 4e-5 * kappa[None]) * np.abs(want) + floor
+    if params.resolved_pipeline() == 'libplacebo' and params.lp_tone == 'ipt' and stage in (2, 3):
+        # the IPT form's LMS -> RGB rows (absolute sums up to 5.3) turn the
+        # LMS values' relative error into an absolute error on channels they
+        # cancel to near zero (saturated colours).  The oracle and the generic
+        # kernel evaluate that form in double, the tile kernel through its PQ
+        # encode / EOTF tables: LMS relative error <= EPS_IPT
+        # encode / EOTF tables: LMS relative error <= EPS_IPT.  Next to black
+        # the stage-1 floor matters more than it does for the max(R,G,B) gain:
+        # the PQ re-encode of a nearly black LMS row is steep (ipt_floor)
+        from ipt_cond import ipt_channel_scale, ipt_floor, lp_encode_spread
+        w2 = want if stage == 2 else oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 2).astype(np.float64)
+        d2 = EPS_IPT * ipt_channel_scale(w2) + ipt_floor(params, lin, w2, 2e-7)
+        tol = tol + (d2 if stage == 2 else lp_encode_spread(params, w2, d2))
     if params.resolved_pipeline() == 'libplacebo' and stage >= 4:
         # after the 8-bit rgba download the values are quantised: 1e-3 holds
         # wherever both sides rounded the download alike; a float-rounding flip
