@@ -282,6 +282,7 @@ def main():
                 # C3 as the reference runs it: the libplacebo branch (rgba8 + lut3d 8-bit, src/utils.py:444-460)
                 ('C3', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 ('C3_cpu_chain', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, pipeline='cpu'), 3840, 2160, 16, 65),
+                ('C3_max_rgb', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, lp_tone='max-rgb'), 3840, 2160, 16, 65),
                 ('C4', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 ('C5', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
                  7680, 4320, 4, 65),
