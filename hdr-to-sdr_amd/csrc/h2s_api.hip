@@ -834,6 +834,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   for (int i = 0; i < 9; i++)
     F->ipt_r2l[i] = (float)(k.ipt_r2l[i] * k.ipt_npl), F->ipt_l2r[i] = (float)(k.ipt_l2r[i] * (p->npl / k.t_white));
   F->pqi_tab = c->d_pqi;
+  F->lut_off = k.lut_enabled ? 0 : 1;
+  for (int i = 0; i < 9; i++) F->m709[i] = k.m709[i];
   curve_fast(k, F);
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
@@ -979,7 +981,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.dbg_lut = c->d_lut;
   F.inv_nm1 = 1.0f / (float)(c->lut_n - 1);
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
-  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.rgba8, s, dbg);
+  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.pipe == h2s::PIPE_LIBPLACEBO ? 1 : 0, s, dbg);
   if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
   return launch_tail(k, nframes, vec, out8, s);
 }
@@ -992,8 +994,11 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
 // tile and 16-byte aligned rows
 static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   const h2s_params& p = c->params;
-  if (!c->fast_enabled || !k.lut_enabled || !h2s::fast_supported(k.tonemap)) return false;
-  if (c->lut_n > 177) return false;
+  if (!c->fast_enabled || !h2s::fast_supported(k.tonemap)) return false;
+  // the LUT off runs on the tile kernel for the libplacebo branch only (the
+  // CPU chain's legacy closed form stays on the generic kernel)
+  if (!k.lut_enabled && k.pipe != h2s::PIPE_LIBPLACEBO) return false;
+  if (k.lut_enabled && c->lut_n > 177) return false;
   if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out) || k.lut_in16) return false;
   return true;
 }
@@ -1261,7 +1266,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   // covers the rest (choose_path / fast_params_ok) and the ragged columns
   const int path = choose_path(c, k, &din, &dout, out8);
   const bool fast = path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL;
-  if (fast && (rc = ensure_lut_yuv(c, k, s))) return rc;
+  if (fast && k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) return rc;
   if (path == H2S_PATH_TWO_PASS && (rc = ensure_chr(c, k))) return rc;
   c->launched = true;
   const bool dyn_peak = c->params.peak_detect && (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE);
@@ -1343,7 +1348,7 @@ int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb,
   // kernel's debug instance then rewrites the tile columns with its own values
   e = h2s::launch_debug(k, stage, dout, s);
   if (e == hipSuccess && (path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL)) {
-    if ((rc = ensure_lut_yuv(c, k, s))) {
+    if (k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) {
       hipStreamSynchronize(s);
       hipFree(scratch);
       return rc;

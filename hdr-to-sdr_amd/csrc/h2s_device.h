@@ -136,6 +136,10 @@ struct FastParams : CurveConsts {
   int lp_ipt;
   float ipt_r2l[9], ipt_l2r[9];
   const float4* pqi_tab;
+  // libplacebo branch with the LUT off (k_tile<..., LP = 1>): libplacebo's own
+  // BT.2020 -> BT.709 conversion (linear matrix, clip) and the nv12 download
+  int lut_off;
+  float m709[9];
   const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)

@@ -544,65 +544,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       if (DBG == 1) dput(r, gg, bl);
       tone<TRC, TM, DESAT>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
       if (DBG == 2) dput(r, gg, bl);
-      float sr, sg, sb;
-      if (LP) {
-        // 255 (BT.1886 encode) rounded to the 8-bit rgba code, then lut3d's
-        // 8-bit coordinate (q / 255) (N-1) in its own operation order: q = 255
-        // lands on N-1 exactly (fract 0: the corners past the lattice edge
-        // get weight 0 and read in-bounds records or the buffer's zero fill)
-        auto q8 = [&](float x) -> float {
+      f3 o;
+      if (LP && F.lut_off) {
+        // LUT off: libplacebo's BT.2020 -> BT.709 matrix on the linear
+        // values, the BT.1886 encode clipped to [0, 1] (no rgba rounding: the
+        // branch downloads nv12), then Y'CbCr at depth q as below
+        auto enc = [&](float x) -> float {
           const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-          return floorf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) + 0.5f);
+          return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
         };
-        const float qr = q8(r), qg = q8(gg), qb = q8(bl);
-        if (DBG == 3) {
-          auto ev = [&](float x) {
-            const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-            return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
-          };
-          dput(ev(r), ev(gg), ev(bl));
-        }
-        sr = qr * F.inv255 * F.nm1, sg = qg * F.inv255 * F.nm1, sb = qb * F.inv255 * F.nm1;
-      } else {
-        // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
-        // s < N-1 and the lattice cell index never needs a clamp
-        sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-        sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-        sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
-      }
-      const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-      const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
-      const bool rg = dr > dg, gb = dg > db, rb = dr > db;
-      const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
-      const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
-      const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
-      const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
-      const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
-      const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0);
-      const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0);
-      const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0);
-      const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
-      const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
-      f3 o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
-      if (LP) {
-        // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
-        // Y'CbCr at depth q in the generic kernel's operation order; o = (luma
-        // code + 0.5, 56 q Cb, 56 q Cr) as the Y'CbCr lattice would give
-        const float R = __builtin_amdgcn_fmed3f(truncf(o.x * 255.0f), 0.0f, 255.0f) * F.inv255;
-        const float G = __builtin_amdgcn_fmed3f(truncf(o.y * 255.0f), 0.0f, 255.0f) * F.inv255;
-        const float B = __builtin_amdgcn_fmed3f(truncf(o.z * 255.0f), 0.0f, 255.0f) * F.inv255;
-        if (DBG == 4) dput(R, G, B);
+        const float R = enc(F.m709[0] * r + F.m709[1] * gg + F.m709[2] * bl);
+        const float G = enc(F.m709[3] * r + F.m709[4] * gg + F.m709[5] * bl);
+        const float B = enc(F.m709[6] * r + F.m709[7] * gg + F.m709[8] * bl);
+        if (DBG == 3 || DBG == 4) dput(R, G, B);
         const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
         o.x = (16.0f + 219.0f * Y) * F.qscale + 0.5f;
         o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
         o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
-      }
-      if (DBG == 3 && !LP) dput(sr * F.inv_nm1, sg * F.inv_nm1, sb * F.inv_nm1);
-      if (DBG == 4 && !LP) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
-        const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
-                     q3 = F.dbg_lut[(base + F.c111) / 12];
-        dput(w0 * q0.x + w1 * q1.x + w2 * q2.x + w3 * q3.x, w0 * q0.y + w1 * q1.y + w2 * q2.y + w3 * q3.y,
-             w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
+      } else {
+        float sr, sg, sb;
+        if (LP) {
+          // 255 (BT.1886 encode) rounded to the 8-bit rgba code, then lut3d's
+          // 8-bit coordinate (q / 255) (N-1) in its own operation order: q = 255
+          // lands on N-1 exactly (fract 0: the corners past the lattice edge
+          // get weight 0 and read in-bounds records or the buffer's zero fill)
+          auto q8 = [&](float x) -> float {
+            const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
+            return floorf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) + 0.5f);
+          };
+          const float qr = q8(r), qg = q8(gg), qb = q8(bl);
+          if (DBG == 3) {
+            auto ev = [&](float x) {
+              const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
+              return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
+            };
+            dput(ev(r), ev(gg), ev(bl));
+          }
+          sr = qr * F.inv255 * F.nm1, sg = qg * F.inv255 * F.nm1, sb = qb * F.inv255 * F.nm1;
+        } else {
+          // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, x_max] (NaN -> 0), so
+          // s < N-1 and the lattice cell index never needs a clamp
+          sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+          sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+          sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, x_max)), 1.0f / 2.4f, log2_nm1));
+        }
+        const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
+        const int base = (int)fmaf(sb - db, stride_b, fmaf(sg - dg, stride_g, (sr - dr) * 12.0f));
+        const bool rg = dr > dg, gb = dg > db, rb = dr > db;
+        const int om = rg ? (rb ? 12 : ob) : (gb ? og : ob);
+        const int ocn = rg ? (gb ? ocb : ocg) : (rb ? ocb : ocr);
+        const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
+        const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
+        const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
+        const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0);
+        const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0);
+        const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0);
+        const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
+        const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
+        o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+        if (LP) {
+          // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
+          // Y'CbCr at depth q in the generic kernel's operation order; o = (luma
+          // code + 0.5, 56 q Cb, 56 q Cr) as the Y'CbCr lattice would give
+          const float R = __builtin_amdgcn_fmed3f(truncf(o.x * 255.0f), 0.0f, 255.0f) * F.inv255;
+          const float G = __builtin_amdgcn_fmed3f(truncf(o.y * 255.0f), 0.0f, 255.0f) * F.inv255;
+          const float B = __builtin_amdgcn_fmed3f(truncf(o.z * 255.0f), 0.0f, 255.0f) * F.inv255;
+          if (DBG == 4) dput(R, G, B);
+          const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
+          o.x = (16.0f + 219.0f * Y) * F.qscale + 0.5f;
+          o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
+          o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
+        }
+        if (DBG == 3 && !LP) dput(sr * F.inv_nm1, sg * F.inv_nm1, sb * F.inv_nm1);
+        if (DBG == 4 && !LP) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
+          const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
+                       q3 = F.dbg_lut[(base + F.c111) / 12];
+          dput(w0 * q0.x + w1 * q1.x + w2 * q2.x + w3 * q3.x, w0 * q0.y + w1 * q1.y + w2 * q2.y + w3 * q3.y,
+               w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
+        }
       }
       if (DBG == 5) dput(o.x - 0.5f, 4.0f * o.y, 4.0f * o.z);
       // luma code (eq applied, shifted) replaces the luma sample this lane read

@@ -221,6 +221,7 @@ FLOAT_CFGS = {
     'C3_bt2390_libplacebo': dict(tonemapper='bt.2390', bits_out=10),
     'C3_bt2390_libplacebo_max_rgb': dict(tonemapper='bt.2390', bits_out=10, lp_tone='max-rgb'),
     'spline_libplacebo_hlg12': dict(tonemapper='spline', bits_in=12, bits_out=12, transfer='arib-std-b67'),
+    'C3_bt2390_libplacebo_lut_off': dict(tonemapper='bt.2390', bits_out=10, lut_enabled=False),
 }
 
 
@@ -309,6 +310,9 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
         from ipt_cond import ipt_channel_scale, ipt_floor, lp_encode_spread
         w2 = want if stage == 2 else oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 2).astype(np.float64)
         d2 = EPS_IPT * ipt_channel_scale(w2) + ipt_floor(params, lin, w2, 2e-7)
+        if stage == 3 and not params.lut_enabled:      # LUT off: the BT.2020 -> 709 matrix first
+            m709 = np.array(oracle.BT2020_TO_BT709)
+            w2, d2 = np.einsum('ck,khw->chw', m709, np.nan_to_num(w2)), np.einsum('ck,khw->chw', np.abs(m709), d2)
         tol = tol + (d2 if stage == 2 else lp_encode_spread(params, w2, d2))
     if params.resolved_pipeline() == 'libplacebo' and stage >= 4:
         # after the 8-bit rgba download the values are quantised: 1e-3 holds

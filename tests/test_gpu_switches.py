@@ -117,11 +117,12 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
     assert params.resolved_pipeline() == 'libplacebo'
     got, want, wh = run_both(tm, params, kind, 128, 64)
     assert_close_int(params, got, want, *wh)
-    # with the LUT on, the branch runs on the tile kernel (k_tile<..., LP = 1>)
-    assert _path(tm, params, 128, 64) == (_abi.PATH_TILE if params.lut_enabled else _abi.PATH_GENERIC)
+    # the branch runs on the tile kernel (k_tile<..., LP = 1>), with the LUT on or off
+    assert _path(tm, params, 128, 64) == _abi.PATH_TILE
 
 
-@pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb'])
+@pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb',
+                                  'bt2390_lut_off_nv12', 'bt2390_max_rgb_lut_off'])
 def test_libplacebo_tile_equals_generic(tm, case):
     """The two kernels of the libplacebo branch against each other (same
     device, same float32 formulas up to the tile kernel's PQ table): the
