@@ -34,6 +34,12 @@ Best mean abs error over the fitted peak, bt2020 / bt601 screenshot model
   6.56, Reinhard and Mobius worse;
 * not separated: knee offset 0.5 (3.41 / 2.31), LUT off (3.25 / 2.12),
   spline (3.21 / 2.33).
+
+And with nothing fitted: the captured C3 chain's own settings
+(tests/golden/filter_chains.json: tonemapping=bt.2390, peak_detect=1) on a
+source without HDR metadata detect the frame's peak (1796 nits) and cap it
+at the 1000-nit default -- the fitted optimum -- and give 3.18 / 2.09 with
+the IPT form against 3.52 / 3.59 with the max(R,G,B) gain.
 """
 import functools
 import os
@@ -140,6 +146,49 @@ def test_no_cpu_chain_curve_matches_it(model):
     assert best_fit(model, (('pipeline', 'cpu'),)) > best + 3.0
     for tm in ('hable', 'reinhard', 'mobius'):
         assert min(mae_oracle(model, tonemapper=tm, peak=p) for p in PEAKS) > best + 1.0
+
+
+def c3_params():
+    """The reference's own C3 chain (captured argv) parsed, at 8-bit output."""
+    import json
+    gold = json.load(open(os.path.join(HERE, 'golden', 'filter_chains.json')))
+    argv = gold['C3']['argv']
+    params, _ = hdr2sdr.parse_filter_chain(argv[argv.index('-filter_complex') + 1])
+    return params.with_(bits_out=8)
+
+
+def mae_dynamic(model, params):
+    fb, sdr = fixture_frame(model)
+    out, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(), fb.buf, fb.width, fb.height)
+    return float(np.abs(decode_yuv8(out[0], fb.width, fb.height, *MODELS[model][1]) - sdr).mean()), peaks[0]
+
+
+@pytest.mark.parametrize('model', sorted(MODELS))
+def test_reference_c3_settings_without_fitting(model):
+    p = c3_params()
+    assert p.peak_detect and p.resolved_pipeline() == 'libplacebo' and p.tonemapper == 'bt.2390'
+    ipt, peak = mae_dynamic(model, p)
+    assert peak == pytest.approx(10.0)        # detected 1796 nits, capped at the 1000-nit default
+    assert ipt < BEST_BOUND[model]
+    assert mae_dynamic(model, p.with_(lp_tone='max-rgb'))[0] > ipt + 0.3
+
+
+@pytest.mark.gpu
+def test_hip_path_with_reference_c3_settings():
+    """The product path with the captured C3 settings (peak detection on the
+    device) on the website pair: the oracle's dynamic output within one
+    8-bit step, and the same error against the reference's SDR frame."""
+    model = 'bt601'
+    fb, sdr = fixture_frame(model)
+    p = c3_params()
+    t = hdr2sdr.Tonemapper(0, p, lattice())
+    dst = hdr2sdr.FrameBatch.empty_numpy(1, fb.width, fb.height, 8)
+    t.process(fb, dst)
+    t.close()
+    want, _ = oracle.process_dynamic(oracle.params_from(p.to_c()), lattice(), fb.buf, fb.width, fb.height)
+    assert (np.abs(dst.buf.astype(np.int64) - want.astype(np.int64)) <= 1).mean() > 0.995
+    got = decode_yuv8(dst.buf[0], fb.width, fb.height, *MODELS[model][1])
+    assert float(np.abs(got - sdr).mean()) < BEST_BOUND[model]
 
 
 @pytest.mark.gpu
