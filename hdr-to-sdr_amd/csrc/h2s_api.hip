@@ -1052,7 +1052,10 @@ static double peak_update(h2s_ctx* c, double fmax, double favg, double static_pe
 // takes every frame's curve in one launch (a record per frame, selected by the
 // tile's frame index), so the chip stays full; the generic kernel and the
 // ragged tail columns go frame by frame.
-static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
+// per-frame max and mean of the PQ-encoded max(R,G,B) for the batch k binds
+// (k_peak_stats_v partials, folded on the host)
+static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, std::vector<double>* fmax,
+                       std::vector<double>* favg) {
   const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
   if (need > c->peak_cap) {
     if (c->d_peak) hipFree(c->d_peak);
@@ -1070,20 +1073,34 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
   const double npx = (double)k.W * k.H;
+  fmax->assign(nframes, 0.0);
+  favg->assign(nframes, 0.0);
+  for (int f = 0; f < nframes; f++) {
+    double mx = 0.0, sum = 0.0;
+    for (int b = 0; b < h2s::PEAK_BLOCKS; b++) {
+      const float2 v = part[(size_t)f * h2s::PEAK_BLOCKS + b];
+      mx = v.x > mx ? v.x : mx;
+      sum += v.y;
+    }
+    (*fmax)[f] = mx;
+    (*favg)[f] = sum / npx;
+  }
+  return 0;
+}
+
+static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
+  std::vector<double> fmx, fav;
+  int rc = frame_stats(c, k, nframes, s, &fmx, &fav);
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
   std::vector<KParams> kfs(nframes, k);
   if (fast) {
     if (c->curve_ev && (e = hipEventSynchronize(c->curve_ev)) != hipSuccess) return hip_fail(c, e, "curve upload");
     c->h_curve.resize(nframes);
   }
   for (int f = 0; f < nframes; f++) {
-    double fmax = 0.0, fsum = 0.0;
-    for (int b = 0; b < h2s::PEAK_BLOCKS; b++) {
-      const float2 v = part[(size_t)f * h2s::PEAK_BLOCKS + b];
-      fmax = v.x > fmax ? v.x : fmax;
-      fsum += v.y;
-    }
     KParams& kf = kfs[f];
-    const double peak = peak_update(c, fmax, fsum / npx, k.peak);
+    const double peak = peak_update(c, fmx[f], fav[f], k.peak);
     bt2390_consts(peak, &kf);
     spline_consts(peak, c->pk_avg, k.sp_contrast, &kf);
     if (fast) curve_fast(kf, &c->h_curve[f]);
@@ -1130,12 +1147,40 @@ int h2s_peak_reset(h2s_ctx* c) {
   return 0;
 }
 
+int h2s_peak_feed(h2s_ctx* c, const double* fmax, const double* favg, int n) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (n < 0 || (n > 0 && (!fmax || !favg))) return fail(c, H2S_E_INVALID_ARG, "bad statistics arrays");
+  KParams k;
+  int rc = prepare(c, &k);
+  if (rc) return rc;
+  for (int i = 0; i < n; i++) peak_update(c, fmax[i], favg[i], k.peak);
+  return 0;
+}
+
 int h2s_peak_state(const h2s_ctx* c, double* max_pq, double* avg_pq, double* peak, int64_t* frames) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (max_pq) *max_pq = c->pk_max;
   if (avg_pq) *avg_pq = c->pk_avg;
   if (peak) *peak = c->pk_peak;
   if (frames) *frames = c->pk_frames;
+  return 0;
+}
+
+int h2s_peak_stats(h2s_ctx* c, const h2s_frames* in, int nframes, double* fmax, double* favg, void* hip_stream) {
+  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  if (nframes < 0 || (nframes > 0 && (!fmax || !favg))) return fail(c, H2S_E_INVALID_ARG, "bad statistics arrays");
+  KParams k;
+  int rc = prepare(c, &k);
+  if (rc) return rc;
+  if ((rc = check_frames(c, in, c->params.bits_in, "input"))) return rc;
+  if (in->location != H2S_LOC_DEVICE) return fail(c, H2S_E_INVALID_ARG, "h2s_peak_stats takes device frames");
+  if (nframes == 0) return 0;
+  DeviceGuard g(c->device);
+  h2s_frames out = *in;                       // geometry only: the statistics read the input planes
+  fill_geometry(&k, in, &out, nframes);
+  std::vector<double> fmx, fav;
+  if ((rc = frame_stats(c, k, nframes, (hipStream_t)hip_stream, &fmx, &fav))) return rc;
+  for (int f = 0; f < nframes; f++) fmax[f] = fmx[f], favg[f] = fav[f];
   return 0;
 }
 

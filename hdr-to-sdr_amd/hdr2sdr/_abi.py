@@ -45,7 +45,7 @@ EXPORTS = (
     'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
     'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
     'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_peak_reset',
-    'h2s_peak_state', 'h2s_set_option', 'h2s_query_path',
+    'h2s_peak_state', 'h2s_peak_stats', 'h2s_peak_feed', 'h2s_set_option', 'h2s_query_path',
 )
 
 
@@ -157,6 +157,9 @@ def lib() -> ctypes.CDLL:
         'h2s_peak_reset': (ctypes.c_int, [c_ctx]),
         'h2s_peak_state': (ctypes.c_int, [c_ctx, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+        'h2s_peak_stats': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+        'h2s_peak_feed': (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
         'h2s_set_option': (ctypes.c_int, [c_ctx, ctypes.c_int, ctypes.c_int64]),
         'h2s_query_path': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.POINTER(H2SFrames)]),
         'h2s_preview_size': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -9,7 +9,13 @@ and run the same kernel on their own HBM.  The only collectives are:
 
 * init: broadcast of the tone-map parameters and the LUT lattice
   (65^3 x 3 fp32 = 3,295,500 B) from rank 0 — RCCL on GPU ranks, gloo on CPU;
-* end: SUM of {pixels, output checksum} and MAX of the elapsed time.
+* end: SUM of {pixels, output checksum} and MAX of the elapsed time;
+* dynamic peak detection only (BT.2390 / spline, peak_detect=1): the peak
+  is smoothed by a recurrence over the whole sequence, which is the one real
+  exchange step.  Each rank measures its own frames' statistics (two floats
+  per frame), all ranks all-gather them, and each replays the frames before
+  its range into its context (h2s_peak_feed) before converting, so the
+  sharded output equals the sequential one (sync_peak_state).
 
 Everything here works with either backend; the CPU tests run it under gloo
 with world_size 2 (tests/test_dist.py).
@@ -103,3 +109,38 @@ def reduce_run(pixels: int, checksum: int, elapsed_s: float, device: Any = 'cpu'
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return int(s[0].item()), int(s[1].item()), float(t[0].item())
+
+
+def gather_peak_stats(fmax: np.ndarray, favg: np.ndarray, nframes: int, device: Any = 'cpu') -> np.ndarray:
+    """All-gather every rank's per-frame (max, mean) statistics into the whole
+    sequence's [nframes, 2] array (ranks own contiguous shard_range blocks)."""
+    import torch
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per = math.ceil(nframes / world) if nframes else 0
+    a, b = shard_range(nframes, world, rank)
+    if len(fmax) != b - a or len(favg) != b - a:
+        raise ValueError(f'rank {rank} owns {b - a} frames, got {len(fmax)} statistics')
+    dev = _comm_device(device)
+    mine = torch.zeros((per, 2), dtype=torch.float64, device=dev)
+    if b > a:
+        mine[:b - a, 0] = torch.as_tensor(np.asarray(fmax, dtype=np.float64), device=dev)
+        mine[:b - a, 1] = torch.as_tensor(np.asarray(favg, dtype=np.float64), device=dev)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    return torch.cat(parts).cpu().numpy()[:nframes]
+
+
+def sync_peak_state(tm: Any, shard: Any, nframes: int, device: Any = 'cpu') -> np.ndarray:
+    """Before converting this rank's shard under dynamic peak detection: its
+    frames' statistics (``tm.peak_stats``) are gathered from every rank and
+    the frames before its range are fed into ``tm``'s smoothing state
+    (``tm.feed_peak``).  Returns the gathered [nframes, 2] statistics."""
+    dist = _dist()
+    a, _ = shard_range(nframes, dist.get_world_size(), dist.get_rank())
+    fmax, favg = tm.peak_stats(shard) if shard.nframes else (np.zeros(0), np.zeros(0))
+    stats = gather_peak_stats(fmax, favg, nframes, device)
+    tm.reset_peak()
+    if a:
+        tm.feed_peak(stats[:a, 0], stats[:a, 1])
+    return stats

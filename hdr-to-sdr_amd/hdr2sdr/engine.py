@@ -154,6 +154,26 @@ class Tonemapper:
         """Start a new sequence: forget the smoothed peak state."""
         self._check(self._L.h2s_peak_reset(self._ctx))
 
+    def peak_stats(self, src: FrameBatch, stream: Any = None) -> 'tuple[np.ndarray, np.ndarray]':
+        """Per-frame (max, mean) of PQ(max R,G,B) of a device batch: the
+        statistics process() folds into the smoothing (h2s_peak_stats)."""
+        n = src.nframes
+        fmax, favg = np.zeros(n), np.zeros(n)
+        di = src.descriptor()
+        self._check(self._L.h2s_peak_stats(self._ctx, ctypes.byref(di), n, fmax.ctypes.data, favg.ctypes.data,
+                                           self._stream_ptr(stream)))
+        return fmax, favg
+
+    def feed_peak(self, fmax: Any, favg: Any) -> None:
+        """Fold frames' statistics into the smoothing state in order, without
+        converting them (h2s_peak_feed): a frame-sharded rank replays the
+        frames before its range."""
+        fmax = np.ascontiguousarray(fmax, dtype=np.float64)
+        favg = np.ascontiguousarray(favg, dtype=np.float64)
+        if fmax.shape != favg.shape or fmax.ndim != 1:
+            raise ValueError('fmax and favg must be 1-D arrays of one length')
+        self._check(self._L.h2s_peak_feed(self._ctx, fmax.ctypes.data, favg.ctypes.data, int(fmax.size)))
+
     def peak_state(self) -> 'dict[str, float]':
         mx, avg, pk = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         n = ctypes.c_int64()

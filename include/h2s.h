@@ -289,6 +289,16 @@ int h2s_query_path(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out);
  *   processed frame, the source peak (units of npl) it gave, and the number
  *   of frames folded in since the reset.  Any pointer may be NULL. */
 int h2s_peak_reset(h2s_ctx *ctx);
+/* Frame-sharded runs (hdr2sdr/dist.py): the smoothing is a recurrence over
+ * the whole sequence, so a rank that owns frames [a, b) first needs the
+ * state frames [0, a) leave.  h2s_peak_stats: the per-frame statistics
+ * h2s_process would fold in (max and mean of PQ(max R,G,B)), for device
+ * frames, without converting them.  h2s_peak_feed: fold n frames' statistics
+ * into the state in order, as h2s_process does.  Gathering every rank's
+ * statistics and feeding the preceding ones makes the sharded output equal
+ * to the sequential one. */
+int h2s_peak_stats(h2s_ctx *ctx, const h2s_frames *in, int nframes, double *fmax, double *favg, void *hip_stream);
+int h2s_peak_feed(h2s_ctx *ctx, const double *fmax, const double *favg, int n);
 int h2s_peak_state(const h2s_ctx *ctx, double *max_pq, double *avg_pq, double *peak, int64_t *frames);
 
 /* ---- preview (src/utils.py:719-765 extract_frame_with_conversion, the

@@ -106,3 +106,86 @@ def test_frame_checksum_is_order_sensitive():
     a = np.arange(12, dtype=np.uint16).reshape(3, 4)
     assert frame_checksum(a, 0) == frame_checksum(a[:2], 0) + frame_checksum(a[2:], 2)
     assert frame_checksum(a[::-1].copy(), 0) != frame_checksum(a, 0)
+
+
+# ---- dynamic peak detection across shards (the one exchange step) ----------
+PW, PH = 64, 32
+
+
+class _OracleTM:
+    """The Tonemapper methods sync_peak_state uses, backed by the oracle
+    (test infrastructure; the GPU form is tests/test_peak_detect.py)."""
+
+    def __init__(self, params, lattice):
+        import oracle
+        self.o, self.p, self.lat = oracle, oracle.params_from(params.to_c()), lattice
+        self.static = oracle.resolved(self.p)[0]
+        self.state = oracle.PeakState()
+
+    def peak_stats(self, shard):
+        return self.o.peak_stats(self.p, shard.buf, PW, PH)
+
+    def reset_peak(self):
+        self.state = self.o.PeakState()
+
+    def feed_peak(self, fmax, favg):
+        for m, a in zip(fmax, favg):
+            self.state.update(float(m), float(a), self.static)
+
+    def convert(self, shard):
+        return self.o.process_dynamic(self.p, self.lat, shard.buf, PW, PH, state=self.state)
+
+
+def _peak_worker(rank, world, port, out_dir, sync):
+    for p in (os.path.join(REPO, 'hdr-to-sdr_amd'), REPO, os.path.join(REPO, 'tests')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    from hdr2sdr import FrameBatch, TonemapParams, generate_lattice
+    from hdr2sdr.dist import frame_checksum, reduce_run, shard_range, sync_peak_state
+    from test_peak_detect import sequence
+
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        buf = sequence(PW, PH)
+        n = buf.shape[0]
+        a, b = shard_range(n, world, rank)
+        tm = _OracleTM(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0), generate_lattice(17))
+        shard = FrameBatch(np.ascontiguousarray(buf[a:b]), PW, PH, 10)
+        if sync:
+            sync_peak_state(tm, shard, n)
+        out, peaks = tm.convert(shard) if b > a else (np.zeros((0, 1)), [])
+        _, total, _ = reduce_run((b - a) * PW * PH, frame_checksum(out, a) if b > a else 0, 0.0)
+        np.save(os.path.join(out_dir, f'p{int(sync)}_{rank}.npy'), np.array([total] + list(peaks), dtype=np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_dynamic_peak_equals_sequential(tmp_path):
+    """6 frames with a scene cut, sharded 3 + 3: with the statistics exchange
+    the sharded run reproduces the sequential peaks and output; without it
+    rank 1 restarts the smoothing at frame 3 and differs."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle
+    from hdr2sdr import TonemapParams, generate_lattice
+    from hdr2sdr.dist import frame_checksum
+    from test_peak_detect import sequence
+
+    buf = sequence(PW, PH)
+    p = oracle.params_from(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0).to_c())
+    seq_out, seq_peaks = oracle.process_dynamic(p, generate_lattice(17), buf, PW, PH)
+    want = frame_checksum(seq_out, 0)
+    world = 2
+    for sync in (1, 0):
+        mp.start_processes(_peak_worker, args=(world, _free_port(), str(tmp_path), bool(sync)), nprocs=world,
+                           join=True, start_method='spawn')
+        res = [np.load(tmp_path / f'p{sync}_{r}.npy') for r in range(world)]
+        peaks = np.concatenate([r[1:] for r in res])
+        if sync:
+            assert int(res[0][0]) == want
+            assert np.allclose(peaks, seq_peaks, rtol=0, atol=0)
+        else:
+            assert int(res[0][0]) != want
+            assert not np.allclose(peaks[3:], seq_peaks[3:])

@@ -131,3 +131,29 @@ def test_gpu_dynamic_peak_hlg12(W, H):
     want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
     assert state['frames'] == 4 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
     assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tmname', ['bt.2390', 'spline'])
+def test_gpu_sharded_peak_state_equals_sequential(tmname):
+    """hdr2sdr.dist.sync_peak_state's device half: a second context that is
+    fed the statistics of the frames before its range (h2s_peak_stats ->
+    h2s_peak_feed) converts its frames bit-identically to one context that
+    walked the whole sequence, and ends in the same smoothing state."""
+    from test_gpu_parity import lattice
+    W, H = 256, 128
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0)
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10).to_torch('cuda')
+    seq = hdr2sdr.Tonemapper(0, params, lattice(65))
+    want = seq(src).to_numpy().buf
+    state = seq.peak_state()
+    fmax, favg = seq.peak_stats(src)
+    seq.close()
+    shard = hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:]), W, H, 10).to_torch('cuda')
+    r1 = hdr2sdr.Tonemapper(0, params, lattice(65))
+    r1.feed_peak(fmax[:3], favg[:3])
+    got = r1(shard).to_numpy().buf
+    assert np.array_equal(got, want[3:])
+    assert r1.peak_state() == state
+    r1.close()
