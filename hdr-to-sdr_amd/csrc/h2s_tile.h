@@ -149,7 +149,7 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // intensity of IPT-PQ instead (three LMS rows encoded through the PQ-encode
 // table, L'M'S' += I' - I decoded through the EOTF table), as the oracle's
 // tone_ipt.
-template <int TRC, int TM, int DESAT>
+template <int TRC, int TM, int DESAT, int LP>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
                                      const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s) {
   if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
@@ -204,7 +204,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       const float ym = fexp2(flog2(fmaxf(y, 0.0f)) * PQ_M1);
       return fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
     };
-    if (F.lp_ipt) {
+    if (LP && F.lp_ipt) {   // (LP instances only: they stage both tables)
       // libplacebo branch, h2s_lp_tone IPT (oracle tone_ipt): the curve on
       // the intensity of IPT-PQ with P and T kept, i.e. L'M'S' += I' - I;
       // encode and decode through the LDS tables (launch-uniform branch; the
@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
       };
       if (DBG == 1) dput(r, gg, bl);
-      tone<TRC, TM, DESAT>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
+      tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
       if (DBG == 2) dput(r, gg, bl);
       f3 o;
       if (LP && F.lut_off) {
