@@ -11,6 +11,7 @@ float path):
 * float intermediates (h2s_debug_float): |gpu - oracle| <= 1e-3 * |oracle| +
   1e-5 absolute floor, per stage.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -579,3 +580,24 @@ def test_concurrent_contexts_on_threads_match_serial():
         for r in range(5):
             assert np.array_equal(outs[i][r], dst.buf), (cfgs[i], r)
         c.close()
+
+
+def test_peak_exchange_and_lp_tone_errors(tm):
+    """h2s_peak_stats takes device frames only; h2s_peak_feed rejects
+    mismatched arrays; an unknown lp_tone is INVALID_ARG at set_params (the
+    ABI validates the raw value, which the Python mirror cannot produce)."""
+    from hdr2sdr import _abi
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True)
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    host = synth_frames('smooth', 2, 128, 64, 10, device='cpu').to_numpy()
+    with pytest.raises(ValueError):
+        tm.peak_stats(host)
+    with pytest.raises(ValueError):
+        tm.feed_peak(np.zeros(3), np.zeros(2))
+    fmax, favg = tm.peak_stats(host.to_torch('cuda'))
+    assert fmax.shape == favg.shape == (2,) and (fmax >= favg).all() and (favg > 0).all()
+    c = params.to_c()
+    c.lp_tone = 7
+    assert tm._L.h2s_set_params(tm._ctx, ctypes.byref(c)) == _abi.H2S_E_INVALID_ARG
+    tm.set_params(params)
