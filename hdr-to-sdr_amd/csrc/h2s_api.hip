@@ -882,9 +882,9 @@ static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
   return 0;
 }
 
-static int prepare(h2s_ctx* c, KParams* k) {
+static int prepare(h2s_ctx* c, KParams* k, bool need_lut = true) {
   if (!c->params_set) return fail(c, H2S_E_INVALID_ARG, "h2s_set_params was not called");
-  if (c->params.lut_enabled && !c->d_lut)
+  if (need_lut && c->params.lut_enabled && !c->d_lut)
     return fail(c, H2S_E_LUT_MISSING, "lut_enabled but no LUT loaded (h2s_set_lut)");
   *k = c->k;
   k->lut = c->d_lut;
@@ -1151,7 +1151,7 @@ int h2s_peak_feed(h2s_ctx* c, const double* fmax, const double* favg, int n) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (n < 0 || (n > 0 && (!fmax || !favg))) return fail(c, H2S_E_INVALID_ARG, "bad statistics arrays");
   KParams k;
-  int rc = prepare(c, &k);
+  int rc = prepare(c, &k, false);  // the statistics need no LUT
   if (rc) return rc;
   for (int i = 0; i < n; i++) peak_update(c, fmax[i], favg[i], k.peak);
   return 0;
@@ -1170,7 +1170,7 @@ int h2s_peak_stats(h2s_ctx* c, const h2s_frames* in, int nframes, double* fmax, 
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
   if (nframes < 0 || (nframes > 0 && (!fmax || !favg))) return fail(c, H2S_E_INVALID_ARG, "bad statistics arrays");
   KParams k;
-  int rc = prepare(c, &k);
+  int rc = prepare(c, &k, false);  // the statistics need no LUT
   if (rc) return rc;
   if ((rc = check_frames(c, in, c->params.bits_in, "input"))) return rc;
   if (in->location != H2S_LOC_DEVICE) return fail(c, H2S_E_INVALID_ARG, "h2s_peak_stats takes device frames");
