@@ -148,10 +148,9 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_INVALID_ARG, "unknown pipeline");
   if (p->lp_tone != H2S_LP_TONE_IPT && p->lp_tone != H2S_LP_TONE_MAX_RGB)
     return fail(c, H2S_E_INVALID_ARG, "unknown lp_tone");
-  if (p->pipeline == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
+  if (p->pipeline == H2S_PIPE_LIBPLACEBO && (p->tonemap < H2S_TM_REINHARD || p->tonemap > H2S_TM_SPLINE))
     return fail(c, H2S_E_UNSUPPORTED,
-                "libplacebo pipeline: only bt.2390 / spline are restated (libplacebo's hable/mobius/reinhard "
-                "curves differ from vf_tonemap's)");
+                "libplacebo pipeline: the reference's operators are reinhard, mobius, hable, bt.2390 and spline");
   if (!isnan(p->knee_offset) && !(p->knee_offset >= 0.5 && p->knee_offset <= 2.0))
     return fail(c, H2S_E_INVALID_ARG, "knee_offset must be in [0.5, 2] (libplacebo's range)");
   if (!isnan(p->target_white) && !(p->target_white > 0 && isfinite(p->target_white)))
@@ -167,6 +166,22 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
 // peak (units of 100 nits) and the SDR target [k->t_black, k->t_white] nits:
 // knee ks = (1 + offset) maxLum - offset, black-point adaptation exponent
 // bp = min(1 / minLum, 4) and gain 1 / (1 + minLum / maxLum (1 - maxLum)^bp)
+// libplacebo's reinhard / hable / mobius in NORM units (1 = target white)
+// for a source peak (units of 100 nits); oracle lp_norm_curve
+void lp_norm_consts(double peak, double tm_param, KParams* k) {
+  const float pk = (float)(peak * 100.0 / k->t_white);
+  k->n_peak = pk;
+  const float ct = isnan(tm_param) ? 0.5f : (float)tm_param;
+  k->n_rein_off = (1.0f - ct) / ct;
+  k->n_rein_scale = (pk + k->n_rein_off) / pk;
+  k->n_hable_inv = 1.0f / hable_h(pk);
+  const float j = isnan(tm_param) ? 0.3f : (float)tm_param;
+  const float a = -j * j * (pk - 1.0f) / (j * j - 2.0f * j + pk);
+  const float b = (j * j - 2.0f * j * pk + pk) / fmaxf(1e-6f, pk - 1.0f);
+  k->n_mob_j = j, k->n_mob_a = a, k->n_mob_b = b;
+  k->n_mob_scale = (b * b + 2.0f * b * j + j * j) / (b - a);
+}
+
 void bt2390_consts(double peak, KParams* k) {
   const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
   const double ml = (pq_encode_d(k->t_white / 10000.0) - smin) / (smax - smin);
@@ -356,6 +371,9 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / k->t_white);
   k->ipt_npl = p->npl / 10000.0, k->ipt_os = 10000.0 / k->t_white;
+  k->lp_norm = lp && p->tonemap >= H2S_TM_REINHARD && p->tonemap <= H2S_TM_MOBIUS ? 1 : 0;
+  k->n_nw = (float)(p->npl / k->t_white);
+  lp_norm_consts(peak, p->tm_param, k);
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
   const double m[9] = {1.6604910021, -0.5876411388, -0.0728498633, -0.1245504745, 1.1328998971,
                        -0.0083494226, -0.0181507634, -0.1005788980, 1.1187296614};
@@ -786,6 +804,9 @@ static void curve_fast(const KParams& k, h2s::CurveConsts* cc) {
     cc->b_bk_a = (float)(-1.0 / R), cc->b_bk_b = (float)((R + C) / R);
     cc->b_bk_c = (float)(R * gain * mn), cc->b_bk_d = (float)((1.0 - gain) * (C + R * mn));
   }
+  cc->n_peak = k.n_peak, cc->n_rein_off = k.n_rein_off, cc->n_rein_scale = k.n_rein_scale;
+  cc->n_hable_inv = k.n_hable_inv, cc->n_mob_j = k.n_mob_j, cc->n_mob_a = k.n_mob_a, cc->n_mob_b = k.n_mob_b;
+  cc->n_mob_scale = k.n_mob_scale;
 }
 
 // FastParams from the resolved KParams (same constants, scales folded)
@@ -835,6 +856,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
     F->ipt_r2l[i] = (float)(k.ipt_r2l[i] * k.ipt_npl), F->ipt_l2r[i] = (float)(k.ipt_l2r[i] * (p->npl / k.t_white));
   F->pqi_tab = c->d_pqi;
   F->lut_off = k.lut_enabled ? 0 : 1;
+  F->n_nw = k.n_nw;
+  F->tw_1e4 = (float)(k.t_white / 10000.0);
   for (int i = 0; i < 9; i++) F->m709[i] = k.m709[i];
   curve_fast(k, F);
   const int n = c->lut_n;
@@ -1103,6 +1126,7 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
     const double peak = peak_update(c, fmx[f], fav[f], k.peak);
     bt2390_consts(peak, &kf);
     spline_consts(peak, c->pk_avg, k.sp_contrast, &kf);
+    lp_norm_consts(peak, c->params.tm_param, &kf);
     if (fast) curve_fast(kf, &c->h_curve[f]);
     for (int p = 0; p < 3; p++) {
       kf.in[p] += f * kf.in_fp[p];
@@ -1314,7 +1338,8 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   if (fast && k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) return rc;
   if (path == H2S_PATH_TWO_PASS && (rc = ensure_chr(c, k))) return rc;
   c->launched = true;
-  const bool dyn_peak = c->params.peak_detect && (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE);
+  const bool dyn_peak = c->params.peak_detect &&
+                        (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE || k.pipe == h2s::PIPE_LIBPLACEBO);
   // the dynamic peak walks frames in order with a host round trip per frame,
   // so it keeps the serial schedule
   if ((host_in || host_out) && nframes > 1 && !dyn_peak && !c->serial_host)

@@ -51,6 +51,10 @@ struct KParams {
   int lp_ipt;             // libplacebo branch: the curve on IPT-PQ intensity (h2s_lp_tone IPT)
   double ipt_r2l[9], ipt_l2r[9];  // BT.2020 RGB -> LMS (HPE), inverse (row-major)
   double ipt_npl, ipt_os;         // npl / 10000, 10000 / target white (double)
+  // libplacebo reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = target white)
+  int lp_norm;                    // the libplacebo branch with one of them
+  float n_peak, n_nw;             // source peak / white; npl / white (npl units -> NORM)
+  float n_rein_off, n_rein_scale, n_hable_inv, n_mob_j, n_mob_a, n_mob_b, n_mob_scale;
   // S3/S4
   int lut_enabled, lut_n, lut_sg, lut_sb;
   float lut_max;
@@ -98,6 +102,8 @@ struct CurveConsts {
   // BT.2390 black-point adaptation on the table coordinate u = e2*R + C:
   // 1 - e2 = u*bk_a + bk_b; u' = gain*u + bk_c*(1 - e2)^bp + bk_d for e2 < 1
   float b_bk_a, b_bk_b, b_bk_c, b_bk_d;
+  // libplacebo reinhard / hable / mobius in NORM units (1 = target white)
+  float n_peak, n_rein_off, n_rein_scale, n_hable_inv, n_mob_j, n_mob_a, n_mob_b, n_mob_scale;
 };
 
 // Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
@@ -140,6 +146,7 @@ struct FastParams : CurveConsts {
   // BT.2020 -> BT.709 conversion (linear matrix, clip) and the nv12 download
   int lut_off;
   float m709[9];
+  float n_nw, tw_1e4;              // npl / target white (npl units -> NORM); target white / 10000
   const CurveConsts* cv_frames;    // dynamic peak: one curve per frame of the launch (else null:
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
@@ -273,6 +280,14 @@ __device__ __forceinline__ double pq_eotf_dd(double e) {
   const double xp = pow(e, 1.0 / (double)PQ_M2);
   return pow(fmax(xp - (double)PQ_C1, 0.0) / ((double)PQ_C2 - (double)PQ_C3 * xp), 1.0 / (double)PQ_M1);
 }
+// libplacebo's reinhard / hable / mobius in NORM units (oracle lp_norm_curve)
+__device__ __forceinline__ float lp_norm_curve(const KParams& P, float x) {
+  x = fminf(fmaxf(x, 0.0f), P.n_peak);
+  if (P.tonemap == 4) return P.n_rein_scale * x / (x + P.n_rein_off);
+  if (P.tonemap == 5) return hable(x) * P.n_hable_inv;
+  return x <= P.n_mob_j ? x : P.n_mob_scale * (x + P.n_mob_a) / (x + P.n_mob_b);
+}
+
 __device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, float& b) {
   const double s = P.ipt_npl;
   const double v0 = fmin((double)r, 1e6) * s, v1 = fmin((double)g, 1e6) * s, v2 = fmin((double)b, 1e6) * s;
@@ -280,7 +295,11 @@ __device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, f
 #pragma unroll
   for (int k = 0; k < 3; k++) q[k] = pq_encode_dd(P.ipt_r2l[3 * k] * v0 + P.ipt_r2l[3 * k + 1] * v1 + P.ipt_r2l[3 * k + 2] * v2);
   const double I = 0.4 * q[0] + 0.4 * q[1] + 0.2 * q[2];
-  const double dI = (double)(P.tonemap == 8 ? spline_pq(P, (float)I) : bt2390_pq(P, (float)I)) - I;
+  double I2;
+  if (P.tonemap == 8) I2 = spline_pq(P, (float)I);
+  else if (P.tonemap == 7) I2 = bt2390_pq(P, (float)I);
+  else I2 = pq_encode_dd((double)lp_norm_curve(P, (float)(pq_eotf_dd(I) * P.ipt_os)) / P.ipt_os);
+  const double dI = I2 - I;
   double l[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) l[k] = pq_eotf_dd(q[k] + dI);
@@ -293,8 +312,15 @@ __device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, f
 // S2: vf_tonemap tonemap() on one linear RGB pixel (units of npl)
 __device__ __forceinline__ void tonemap_px(const KParams& P, float& r, float& g, float& b) {
   float sig, sig_orig;
-  if (P.lp_ipt && (P.tonemap == 7 || P.tonemap == 8)) {
+  if (P.lp_ipt) {   // set on the libplacebo branch only
     tone_ipt(P, r, g, b);
+    return;
+  }
+  if (P.lp_norm) {  // libplacebo branch, max(R,G,B) gain (oracle tonemap_px)
+    r = fminf(r, 1e6f), g = fminf(g, 1e6f), b = fminf(b, 1e6f);
+    sig = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
+    const float k = lp_norm_curve(P, sig * P.n_nw) / sig;
+    r *= k, g *= k, b *= k;
     return;
   }
   if (P.tonemap == 8 /* SPLINE */) {

@@ -152,6 +152,39 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 template <int TRC, int TM, int DESAT, int LP>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
                                      const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s) {
+  if (LP && TM >= 4 && TM <= 6) {
+    // libplacebo's reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = the
+    // target white; oracle lp_norm_curve), on the IPT intensity or as the
+    // max(R,G,B) gain; the frame's constants come from its curve record
+    auto curve = [&](float x) -> float {
+      x = __builtin_amdgcn_fmed3f(x, 0.0f, C.n_peak);
+      if (TM == 4) return C.n_rein_scale * x / (x + C.n_rein_off);
+      if (TM == 5) return hable(x) * C.n_hable_inv;
+      return x <= C.n_mob_j ? x : C.n_mob_scale * (x + C.n_mob_a) / (x + C.n_mob_b);
+    };
+    const float R = fminf(r, 1e6f), G = fminf(g, 1e6f), B = fminf(b, 1e6f);
+    if (F.lp_ipt) {
+      const float q0 = pqi(pqi_lds, F.ipt_r2l[0] * R + F.ipt_r2l[1] * G + F.ipt_r2l[2] * B);
+      const float q1 = pqi(pqi_lds, F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
+      const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
+      const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
+      const float x = pq_z(pq_lds, fmaf(I, (float)PQ_SEG, 1.0f)) * F.tw_fold;     // NORM
+      const float I2 = pqi(pqi_lds, curve(x) * F.tw_1e4);
+      const float du = fmaf(I2 - I, (float)PQ_SEG, 1.0f);
+      auto lz = [&](float q) {
+        return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f));
+      };
+      const float l0 = lz(q0), l1 = lz(q1), l2 = lz(q2);
+      r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
+      g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
+      b = F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2;
+    } else {
+      const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(R, G), B), 1e-6f);
+      const float k = curve(sig * F.n_nw) / sig;
+      r = R * k, g = G * k, b = B * k;
+    }
+    return;
+  }
   if (TM == 7 || TM == 8) {  // BT.2390 / spline (PQ-domain curves, no desat)
     // PQ input: the curve straight into pq_z's table coordinate u = e4*PQ_SEG
     // + 1 (the output scale and offset are folded into the polynomial
@@ -511,7 +544,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
     // frame, read through the scalar cache; the frame index is block-uniform)
     CurveConsts cv = F;
-    if ((TM == 7 || TM == 8) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
+    if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
       tile_next(F, geo);
@@ -695,6 +728,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   X(0, 8, 0, 0)       \
   X(0, 7, 0, 1)       \
   X(0, 8, 0, 1)       \
+  X(0, 4, 0, 1)       \
+  X(0, 5, 0, 1)       \
+  X(0, 6, 0, 1)       \
   X(1, 4, 0, 0)       \
   X(1, 4, 1, 0)       \
   X(1, 4, 2, 0)       \
@@ -707,7 +743,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   X(1, 7, 0, 0)       \
   X(1, 8, 0, 0)       \
   X(1, 7, 0, 1)       \
-  X(1, 8, 0, 1)
+  X(1, 8, 0, 1)       \
+  X(1, 4, 0, 1)       \
+  X(1, 5, 0, 1)       \
+  X(1, 6, 0, 1)
 
 // one DBG value's instances (0 = product kernels; 1..5 = the debug instance
 // for that h2s_stage), explicitly instantiated in exactly one .hip each

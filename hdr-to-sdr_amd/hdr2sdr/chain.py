@@ -39,6 +39,9 @@ FFMPEG_CONVERT_FILTER = (
 # engine runs both natively on the GPU (BT.2390 EETF and libplacebo's spline
 # curve, restated in libh2s; parity unpinned).
 GPU_ONLY_TONEMAPPERS = {'bt.2390', 'spline'}
+# every operator of the reference's TONEMAP list reaches libplacebo when GPU
+# tone mapping is on (src/utils.py:16; src/ffmpeg_command.py:236-239)
+LIBPLACEBO_TONEMAPPERS = {'reinhard', 'mobius', 'hable', 'bt.2390', 'spline'}
 
 _TM_NAMES = {
     'none': _abi.TM_NONE, 'linear': _abi.TM_LINEAR, 'gamma': _abi.TM_GAMMA,
@@ -115,9 +118,9 @@ class TonemapParams:
                             ('pipeline', _PIPELINE), ('chroma_edge', _EDGE), ('lut_input', _LUT_IN), ('lp_tone', _LP_TONE)):
             if getattr(self, name) not in table:
                 raise ValueError(f'unknown {name} {getattr(self, name)!r}; expected one of {sorted(table)}')
-        if self.pipeline == 'libplacebo' and tm not in GPU_ONLY_TONEMAPPERS:
-            # libplacebo's own hable/mobius/reinhard curves are not restated
-            raise ValueError(f'libplacebo tonemapping={tm} is not supported (only bt.2390 / spline)')
+        if self.pipeline == 'libplacebo' and tm not in LIBPLACEBO_TONEMAPPERS:
+            raise ValueError(f'libplacebo tonemapping={tm} is not supported '
+                             f'(the reference names {sorted(LIBPLACEBO_TONEMAPPERS)})')
         if self.bits_in not in (10, 12):
             raise ValueError(f'bits_in must be 10 or 12, got {self.bits_in}')
         if self.bits_out not in (8, 10, 12):
@@ -279,18 +282,19 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             tm = kv.get('tonemapping')
             if tm is None:
                 raise ValueError('libplacebo stage without tonemapping=')
-            if not is_gpu_only_tonemapper(tm):
-                # the reference emits libplacebo chains for every operator
-                # with use_gpu (src/ffmpeg_command.py:119, :236); libplacebo's
-                # own hable/mobius/reinhard curves differ from vf_tonemap's
-                # and are not restated: refuse rather than mis-map them
-                raise ValueError(f'libplacebo tonemapping={tm} is not supported (only bt.2390 / spline)')
+            if tm.lower() not in LIBPLACEBO_TONEMAPPERS:
+                # the reference emits libplacebo chains for each of its five
+                # operators with use_gpu (src/ffmpeg_command.py:119, :236;
+                # TONEMAP, src/utils.py:16): libplacebo's own reinhard / hable /
+                # mobius (NORM scaling) are restated beside bt.2390 / spline
+                raise ValueError(f'libplacebo tonemapping={tm} is not supported '
+                                 f'(the reference names {sorted(LIBPLACEBO_TONEMAPPERS)})')
             seen_linear = True
             kw['tonemapper'] = tm.lower()
             kw['desat'] = 0.0
             kw['pipeline'] = 'libplacebo'
             # peak_detect=1 (src/utils.py:448): per-frame detected, temporally
-            # smoothed source peak; libh2s restates it for BT.2390 and spline
+            # smoothed source peak (every libplacebo operator: it sets the source range)
             kw['peak_detect'] = kv.get('peak_detect', '0') in ('1', 'true')
         elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
             continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)

@@ -87,6 +87,7 @@ typedef struct {
   double out_scale;     /* curve output (PQ-normalised linear) -> units of tw */
   double enc_a, enc_b;  /* libplacebo BT.1886 encode: (x / a)^(1/2.4) - b   */
   int ipt;              /* libplacebo branch: curve on IPT-PQ intensity      */
+  double n_peak;        /* libplacebo NORM curves: source peak / target white */
   double r2l[3][3], l2r[3][3]; /* BT.2020 RGB -> LMS (HPE), inverse           */
   int dither;           /* 1: ordered dither at the swscale 8-bit quantiser */
 } ocfg;
@@ -254,6 +255,50 @@ static float spline_sig(const ocfg *c, float sig) {
 
 #define MIX(x, y, a) (x) * (1 - (a)) + (y) * (a)
 
+/* libplacebo's reinhard / hable / mobius (tone_mapping.c, scaling PL_HDR_NORM):
+ * the reference's libplacebo chains name them whenever GPU tone mapping is on
+ * (src/ffmpeg_command.py:236-239, src/utils.py:16).  Restated from the
+ * published functions; libplacebo is absent: PARITY UNPINNED.  In NORM units
+ * (1.0 = the SDR target white) the input is clipped to the source range
+ * [0, peak / white] (the LUT's domain) and mapped so that the source peak
+ * lands on the white: reinhard x (peak + o)/peak / (x + o), o = (1 - c)/c,
+ * contrast c = tm_param (default 0.5); hable(x) / hable(peak) with Hable's
+ * constants; mobius with knee j = tm_param (default 0.3), identity below j.
+ * Below the target black the BT.1886 encode clips to code 0, so a clamp of
+ * the curve to [black, white] would not change any output. */
+static float lp_norm_curve(const ocfg *c, float x) {
+  const float pk = (float)c->n_peak;
+  x = fminf(fmaxf(x, 0.0f), pk);
+  switch (c->p->tonemap) {
+    case H2S_TM_REINHARD: {
+      const float ct = isnan(c->p->tm_param) ? 0.5f : (float)c->p->tm_param;
+      const float off = (1.0f - ct) / ct, scale = (pk + off) / pk;
+      return scale * x / (x + off);
+    }
+    case H2S_TM_HABLE:
+      return hable(x) / hable(pk);
+    default: {  /* MOBIUS */
+      const float j = isnan(c->p->tm_param) ? 0.3f : (float)c->p->tm_param;
+      if (x <= j) return x;
+      const float a = -j * j * (pk - 1.0f) / (j * j - 2.0f * j + pk);
+      const float b = (j * j - 2.0f * j * pk + pk) / fmaxf(1e-6f, pk - 1.0f);
+      const float scale = (b * b + 2.0f * b * j + j * j) / (b - a);
+      return scale * (x + a) / (x + b);
+    }
+  }
+}
+
+/* the libplacebo branch's curve on a PQ-domain intensity (the IPT form, in
+ * double around the float curves) */
+static double lp_curve_pq_d(const ocfg *c, double e) {
+  switch (c->p->tonemap) {
+    case H2S_TM_BT2390: return bt2390_pq(c, (float)e);
+    case H2S_TM_SPLINE: return spline_pq_f(c, (float)e);
+    default:
+      return pq_encode_d((double)lp_norm_curve(c, (float)(pq_eotf_dd(e) * (10000.0 / c->tw))) * (c->tw / 10000.0));
+  }
+}
+
 /* libplacebo branch, h2s_params.lp_tone = IPT: the PQ-domain curve on the
  * intensity of IPT-PQ, P and T kept.  Linear BT.2020 R'G'B' (npl units) ->
  * LMS (HPE of XYZ, D65-normalised so that a neutral has L = M = S = Y) in
@@ -273,8 +318,7 @@ static rgbf tone_ipt(const ocfg *c, rgbf in) {
   double q[3];
   for (int k = 0; k < 3; k++) q[k] = pq_encode_d(c->r2l[k][0] * v[0] + c->r2l[k][1] * v[1] + c->r2l[k][2] * v[2]);
   const double I = 0.4 * q[0] + 0.4 * q[1] + 0.2 * q[2];
-  const double dI =
-      (double)(c->p->tonemap == H2S_TM_SPLINE ? spline_pq_f(c, (float)I) : bt2390_pq(c, (float)I)) - I;
+  const double dI = lp_curve_pq_d(c, I) - I;
   double l[3];
   for (int k = 0; k < 3; k++) l[k] = pq_eotf_dd(q[k] + dI);
   const double os = c->out_scale;
@@ -288,7 +332,17 @@ static rgbf tonemap_px(const ocfg *c, rgbf in) {
   rgbf o = in;
   float sig, sig_orig;
   int tm = c->p->tonemap;
-  if (c->ipt && (tm == H2S_TM_SPLINE || tm == H2S_TM_BT2390)) return tone_ipt(c, in);
+  if (c->ipt) return tone_ipt(c, in);  /* only set on the libplacebo branch */
+  if (c->pipe == H2S_PIPE_LIBPLACEBO && tm >= H2S_TM_REINHARD && tm <= H2S_TM_MOBIUS) {
+    /* lp_tone = MAX_RGB: the NORM curve's gain on max(R,G,B) (inputs capped
+     * at 1e6 npl as in the IPT form: inf * 0 would be NaN) */
+    o.r = fminf(o.r, 1e6f), o.g = fminf(o.g, 1e6f), o.b = fminf(o.b, 1e6f);
+    sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
+    const float nw = (float)(c->p->npl / c->tw);                   /* npl units -> NORM */
+    const float k = lp_norm_curve(c, sig * nw) / sig;             /* output in units of the target white */
+    o.r *= k, o.g *= k, o.b *= k;
+    return o;
+  }
   if (tm == H2S_TM_SPLINE) {
     sig = fmaxf(fmaxf(fmaxf(o.r, o.g), o.b), 1e-6f);
     float s2 = spline_sig(c, sig);
@@ -598,8 +652,8 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   c->pipe = p->pipeline;
   if (c->pipe == H2S_PIPE_AUTO)
     c->pipe = (p->tonemap == H2S_TM_BT2390 || p->tonemap == H2S_TM_SPLINE) ? H2S_PIPE_LIBPLACEBO : H2S_PIPE_CPU_CHAIN;
-  if (c->pipe == H2S_PIPE_LIBPLACEBO && p->tonemap != H2S_TM_BT2390 && p->tonemap != H2S_TM_SPLINE)
-    return H2S_E_UNSUPPORTED; /* libplacebo's own hable/mobius/reinhard curves are not restated */
+  if (c->pipe == H2S_PIPE_LIBPLACEBO && (p->tonemap < H2S_TM_REINHARD || p->tonemap > H2S_TM_SPLINE))
+    return H2S_E_UNSUPPORTED; /* the reference's libplacebo chains name only its five TONEMAP operators */
   c->rgba8 = c->pipe == H2S_PIPE_LIBPLACEBO && p->lut_enabled;
   /* quantisation depth: the CPU chain's eq forces yuv420p (compat8); the
    * libplacebo branch with the LUT and gamma 1 has no eq, so its rgba frame
@@ -678,6 +732,7 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
     c->enc_b = lb / (1.0 - lb);
   }
   c->ipt = lp && p->lp_tone == H2S_LP_TONE_IPT;
+  c->n_peak = peak * 100.0 / c->tw;
   ipt_matrices(c->r2l, c->l2r);
   /* BT.2390 constants (libplacebo bt2390): source [0, peak*100 nits] and
    * target [black, white] in PQ, normalised to the source range */

@@ -123,14 +123,21 @@ def test_libplacebo_spline_chain_parses_to_native_spline():
 
 
 @pytest.mark.parametrize('tm', ['hable', 'mobius', 'reinhard'])
-def test_libplacebo_chain_with_vf_tonemap_curve_names_is_rejected(tm):
-    """The reference emits a libplacebo chain for every operator when use_gpu
-    is set (src/ffmpeg_command.py:119, :236), but libplacebo's hable / mobius /
-    reinhard are different curves from vf_tonemap's of the same name and are
-    not restated: such a chain must fail loudly, not run the wrong operator."""
+def test_libplacebo_chain_with_cpu_operator_names_parses(tm):
+    """The reference emits a libplacebo chain for every operator when GPU
+    tone mapping is on (src/ffmpeg_command.py:119, :236): libplacebo's own
+    reinhard / hable / mobius (NORM scaling, restated) on the libplacebo
+    pipeline, not vf_tonemap's curves of the same name."""
     chain = (f'[0:v:0]format=p010,hwupload,libplacebo=w=iw:h=ih:tonemapping={tm}:colorspace=bt709:'
              'color_primaries=auto:color_trc=bt709:range=tv:peak_detect=1:format=rgba,hwdownload,format=rgba,'
              'lut3d=file=<LUT>:interp=tetrahedral,setparams=color_primaries=bt709:color_trc=bt709:'
              'colorspace=bt709[vout]')
+    p, _ = parse_filter_chain(chain)
+    assert p.tonemapper == tm and p.pipeline == 'libplacebo' and p.peak_detect and p.desat == 0.0
+
+
+@pytest.mark.parametrize('tm', ['clip', 'linear', 'gamma'])
+def test_libplacebo_chain_with_other_operators_is_rejected(tm):
+    chain = f'libplacebo=w=iw:h=ih:tonemapping={tm}:peak_detect=1:format=rgba,hwdownload,format=rgba'
     with pytest.raises(ValueError):
         parse_filter_chain(chain)

@@ -223,6 +223,7 @@ FLOAT_CFGS = {
     'C3_bt2390_libplacebo_max_rgb': dict(tonemapper='bt.2390', bits_out=10, lp_tone='max-rgb'),
     'spline_libplacebo_hlg12': dict(tonemapper='spline', bits_in=12, bits_out=12, transfer='arib-std-b67'),
     'C3_bt2390_libplacebo_lut_off': dict(tonemapper='bt.2390', bits_out=10, lut_enabled=False),
+    'hable_libplacebo': dict(tonemapper='hable', bits_out=10, pipeline='libplacebo'),
 }
 
 

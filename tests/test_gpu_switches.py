@@ -107,6 +107,12 @@ LP_CASES = {
     'spline_max_rgb_hlg12': dict(tonemapper='spline', lp_tone='max-rgb', bits_in=12, bits_out=12,
                                  transfer='arib-std-b67'),
     'bt2390_max_rgb_lut_off': dict(tonemapper='bt.2390', lp_tone='max-rgb', lut_enabled=False),
+    # libplacebo's own reinhard / hable / mobius (NORM scaling)
+    'lp_hable': dict(tonemapper='hable', pipeline='libplacebo'),
+    'lp_mobius_max_rgb': dict(tonemapper='mobius', pipeline='libplacebo', lp_tone='max-rgb'),
+    'lp_reinhard_hlg12_lut_off': dict(tonemapper='reinhard', pipeline='libplacebo', bits_in=12, bits_out=12,
+                                      transfer='arib-std-b67', lut_enabled=False),
+    'lp_mobius_gamma13': dict(tonemapper='mobius', pipeline='libplacebo', gamma=1.3),
 }
 
 
@@ -117,12 +123,14 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
     assert params.resolved_pipeline() == 'libplacebo'
     got, want, wh = run_both(tm, params, kind, 128, 64)
     assert_close_int(params, got, want, *wh)
-    # the branch runs on the tile kernel (k_tile<..., LP = 1>), with the LUT on or off
+    # every operator of the branch runs on the tile kernel (k_tile<..., LP = 1>),
+    # with the LUT on or off
     assert _path(tm, params, 128, 64) == _abi.PATH_TILE
 
 
 @pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb',
-                                  'bt2390_lut_off_nv12', 'bt2390_max_rgb_lut_off'])
+                                  'bt2390_lut_off_nv12', 'bt2390_max_rgb_lut_off', 'lp_hable', 'lp_mobius_max_rgb',
+                                  'lp_reinhard_hlg12_lut_off'])
 def test_libplacebo_tile_equals_generic(tm, case):
     """The two kernels of the libplacebo branch against each other (same
     device, same float32 formulas up to the tile kernel's PQ table): the
@@ -187,12 +195,13 @@ def test_libplacebo_chain_string_selects_the_branch(tm):
     assert_close_int(params, got, want, *wh)
 
 
+@pytest.mark.parametrize('tmname', ['bt.2390', 'mobius'])
 @pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])
-def test_libplacebo_dynamic_peak(W, H):
+def test_libplacebo_dynamic_peak(W, H, tmname):
     """peak_detect=1 (src/utils.py:448) on the libplacebo branch, across calls."""
     from test_peak_detect import sequence
     buf = sequence(W, H)
-    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0, pipeline='libplacebo')
     t = hdr2sdr.Tonemapper(0, params, lattice(65))
     got = []
     for a, b in ((0, 2), (2, 6)):

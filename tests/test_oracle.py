@@ -343,3 +343,33 @@ def test_rgb48_lut_stage_values_are_16bit():
 def test_lut_input_rejects_unknown():
     with pytest.raises(ValueError):
         hdr2sdr.TonemapParams(lut_input='rgb24')
+
+
+# ---- libplacebo's reinhard / hable / mobius (PL_HDR_NORM, PARITY UNPINNED) --
+def _hable_ref(x):
+    a, b, c, d, e, f = 0.15, 0.50, 0.10, 0.20, 0.02, 0.30
+    return (x * (x * a + b * c) + d * e) / (x * (x * a + b) + d * f) - e / f
+
+
+@pytest.mark.parametrize('tm', ['reinhard', 'hable', 'mobius'])
+@pytest.mark.parametrize('peak', [10.0, 40.0])
+def test_libplacebo_norm_curves_match_independent_transcription(tm, peak):
+    """In NORM units (1 = the 203-nit SDR white) the source peak lands on the
+    white; reinhard with contrast 0.5, hable over hable(peak), mobius with knee
+    0.3 (identity below it); inputs above the source peak clip to it."""
+    p = params(tonemap=tm, pipeline=PIPE_LP, peak=peak)
+    pk = peak * 100.0 / 203.0
+    for sig in (0.01, 0.1, 0.5, 1.0, 2.0, 5.0, peak, 2 * peak):    # units of npl (100 nits)
+        x = min(sig * 100.0 / 203.0, pk)
+        if tm == 'reinhard':
+            off = 1.0
+            want = (pk + off) / pk * x / (x + off)
+        elif tm == 'hable':
+            want = _hable_ref(x) / _hable_ref(pk)
+        else:
+            j = 0.3
+            a = -j * j * (pk - 1) / (j * j - 2 * j + pk)
+            b = (j * j - 2 * j * pk + pk) / max(1e-6, pk - 1)
+            want = x if x <= j else (b * b + 2 * b * j + j * j) / (b - a) * (x + a) / (x + b)
+        assert oracle.tone_curve(p, sig) == pytest.approx(want, rel=2e-5, abs=1e-7), (tm, sig)
+    assert oracle.tone_curve(p, peak) == pytest.approx(1.0, rel=1e-5)
