@@ -36,8 +36,9 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
-// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma.  lp: the
-// libplacebo branch's rgba8 form (BT.2390 / spline only).  dbg: 0 = the
+// desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma (vf_tonemap's; the
+// libplacebo curves have none).  lp: the libplacebo branch (every operator).
+// dbg: 0 = the
 // product kernel; 1..5 = its debug instance for that h2s_stage (F.dbg set)
 hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
@@ -45,8 +46,7 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
   const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
-  if (tm == 7 || tm == 8) desat = 0;
-  else lp = 0;
+  if (tm == 7 || tm == 8 || lp) desat = 0;
   switch (dbg) {
     case 0: return launch_tile<0>(F, trc, tm, desat, lp, grid, lds, s);
     case 1: return launch_tile<1>(F, trc, tm, desat, lp, grid, lds, s);
