@@ -150,7 +150,9 @@ enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
  * CPU_CHAIN: FFMPEG_CONVERT_FILTER (src/utils.py:38-42): zscale -> tonemap ->
  *   zscale -> lut3d (float) -> yuv420p -> eq -> -pix_fmt.
  * LIBPLACEBO: build_libplacebo_filter (src/utils.py:392-471) with the LUT on:
- *   libplacebo tone map (BT.2390 / spline) -> BT.1886 encode against the SDR
+ *   libplacebo tone map (BT.2390, spline, or libplacebo's own reinhard /
+ *   hable / mobius, which the reference also routes there with GPU tone
+ *   mapping on) -> BT.1886 encode against the SDR
  *   target -> 8-bit rgba download -> lut3d's 8-bit path (truncating output) ->
  *   Y'CbCr at the output depth (gamma = 1; the chain has no eq) or, with
  *   eq=gamma, yuv420p -> eq -> -pix_fmt.  With the LUT off the branch keeps
