@@ -283,6 +283,7 @@ def main():
                 ('C3', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 ('C3_cpu_chain', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, pipeline='cpu'), 3840, 2160, 16, 65),
                 ('C3_max_rgb', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, lp_tone='max-rgb'), 3840, 2160, 16, 65),
+                ('C2_libplacebo', dict(tonemapper='hable', gamma=2.2, bits_out=10, pipeline='libplacebo'), 3840, 2160, 16, 65),
                 ('C4', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 ('C5', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
                  7680, 4320, 4, 65),
