@@ -367,8 +367,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base
 
 // one tile's global loads, held in registers between issue and the LDS commit
 struct TileRegs {
-  uint4 ya, ua, va;
-  unsigned uh, vh;
+  uint4 ya, ua;     // luma chunk; chroma chunk of plane pc (threads tc < 72)
+  unsigned uh;      // the chroma chunk's right-halo sample
 };
 
 struct TileGeo {
@@ -407,30 +407,60 @@ __device__ __forceinline__ void tile_next(const FastParams& F, TileGeo& g) {
   }
 }
 
+// per-lane byte offsets of a tile's loads and stores relative to the tile's
+// origin, fixed for the whole launch (the strides do not change): interior
+// tiles then address with one scalar origin (soffset) and no per-lane
+// arithmetic
+struct LaneOfs {
+  int y, u;        // loads: luma row yr, chunk yc; chroma row clr, chunk ccx of plane pc
+  int sy, sc;      // stores: luma row / 8-sample chunk; chroma row of plane pl
+};
+
+__device__ __forceinline__ LaneOfs lane_ofs(const FastParams& F, int t) {
+  LaneOfs L;
+  L.y = (t >> 3) * (int)F.in_ls[0] + 16 * (t & 7);
+  const int pc = (t >> 7) & 1, tc = t & 127;
+  L.u = (tc >> 2) * (int)F.in_ls[1 + pc] + 16 * (tc & 3);
+  const int sb = F.out8 ? 8 : 16;
+  L.sy = (t >> 3) * (int)F.out_ls[0] + sb * (t & 7);
+  const int pl = (t >> 6) & 1, rem = t & 63;
+  L.sc = (rem >> 2) * (int)F.out_ls[1 + pl] + sb * (rem & 3);
+  return L;
+}
+
 // issue (do not wait for) the loads of one tile: luma 64 x 32 (one 16-byte
 // load per thread) and chroma rows cy0-1 .. cy0+16 (18 rows x 4 chunks of 8
-// samples + 1 right-halo sample; threads 0..71).  One thread loads the same
-// chunk of both planes, so each buffer resource stays wave-uniform (a per-lane
-// choice of resource becomes a waterfall loop).
-__device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t) {
+// samples + 1 right-halo sample): plane U on threads 0..71, plane V on threads
+// 128..199, so waves 0-1 and 2-3 share the chroma work and the plane (hence the
+// buffer resource) is wave-uniform.  Tiles whose rows (and chroma
+// halo) lie inside the frame take the lane offsets of LaneOfs plus a scalar
+// origin; border tiles clamp per lane.  The chroma registers of threads >= 72
+// are left undefined (never committed).
+__device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t, const LaneOfs& L) {
   const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], F.in_bytes[0]);
   const int yr = t >> 3, yc = t & 7;
   TileRegs r;
-  r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                       iy, (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), 0, NT));
-  r.ua = r.va = make_uint4(0, 0, 0, 0);
-  r.uh = r.vh = 0;
-  if (t < 72) {
-    const __amdgpu_buffer_rsrc_t iu = plane_rsrc(F.in[1] + g.f * F.in_fp[1], F.in_bytes[1]);
-    const __amdgpu_buffer_rsrc_t iv = plane_rsrc(F.in[2] + g.f * F.in_fp[2], F.in_bytes[2]);
-    const int clr = t >> 2, ccx = t & 3;
-    const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
-    const int hx = 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
-    const int ou = row * (int)F.in_ls[1], ov = row * (int)F.in_ls[2];
-    r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iu, ou + 2 * (g.cx0 + 8 * ccx), 0, NT));
-    r.va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iv, ov + 2 * (g.cx0 + 8 * ccx), 0, NT));
-    r.uh = __builtin_amdgcn_raw_buffer_load_b16(iu, ou + hx, 0, 0);
-    r.vh = __builtin_amdgcn_raw_buffer_load_b16(iv, ov + hx, 0, 0);
+  if (g.py0 + TBH <= F.H)   // block-uniform
+    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         iy, L.y, g.py0 * (int)F.in_ls[0] + 2 * g.px0, NT));
+  else
+    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         iy, (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), 0, NT));
+  const int pc = __builtin_amdgcn_readfirstlane(t >> 7), tc = t & 127;
+  if (tc < 72) {
+    const __amdgpu_buffer_rsrc_t ic = plane_rsrc(F.in[1 + pc] + g.f * F.in_fp[1 + pc], F.in_bytes[1 + pc]);
+    const int ls = (int)F.in_ls[1 + pc];
+    if (g.cy0 >= 1 && g.cy0 + CBH + 1 <= F.ch && g.cx0 + CBW + 1 <= F.cw) {   // block-uniform
+      const int so = (g.cy0 - 1) * ls + 2 * g.cx0;
+      r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, L.u, so, NT));
+      r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, L.u + 16, so, 0);
+    } else {
+      const int clr = tc >> 2, ccx = tc & 3;
+      const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
+      const int hx = 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
+      r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, row * ls + 2 * (g.cx0 + 8 * ccx), 0, NT));
+      r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, row * ls + hx, 0, 0);
+    }
   }
   return r;
 }
@@ -468,7 +498,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
   // ---- prologue: first tile + tables, all issued before any wait ----
   TileGeo geo = tile_geo(F, tile);
-  TileRegs cur = tile_load(F, geo, t);
+  const LaneOfs lofs = lane_ofs(F, t);
+  TileRegs cur = tile_load(F, geo, t, lofs);
   const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
   const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * t, 0, 0);  // out of range -> 0
   float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -522,23 +553,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
       *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
     }
-    if (t < 72) {
+    if ((t & 127) < 72) {
       // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
       // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float
-      auto put = [&](const uint4 a, unsigned h, float* plane) {
+      auto put = [&](const uint4 a, unsigned h, float* plane, int tt) {
         float v[9];
         unpack8(a, v);
         v[8] = (float)h;
 #pragma unroll
         for (int k = 0; k < 9; k++) v[k] -= cmid;
-        float* d = plane + (t >> 2) * HST + 16 * (t & 3);
+        float* d = plane + (tt >> 2) * HST + 16 * (tt & 3);
 #pragma unroll
         for (int k = 0; k < 4; k++)
           *reinterpret_cast<float4*>(d + 4 * k) =
               make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
       };
-      put(cur.ua, cur.uh, hrow[0]);
-      put(cur.va, cur.vh, hrow[1]);
+      put(cur.ua, cur.uh, hrow[__builtin_amdgcn_readfirstlane(t >> 7)], t & 127);
     }
     const TileGeo g = geo;
     // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
@@ -548,7 +578,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
       tile_next(F, geo);
-      cur = tile_load(F, geo, t);        // in flight during this tile's compute
+      cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
     __syncthreads();
 
@@ -673,20 +703,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       if (g.py0 + r < F.H) {
         const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
         const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
-        const int off = (g.py0 + r) * (int)F.out_ls[0];
+        const int so = g.py0 * (int)F.out_ls[0];
         if (F.out8)
           __builtin_amdgcn_raw_buffer_store_b64(
               __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
-              oy_, off + g.px0 + 8 * c, 0, NT);
+              oy_, lofs.sy, so + g.px0, NT);
         else
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
-              oy_, off + 2 * (g.px0 + 8 * c), 0, NT);
+              oy_, lofs.sy, so + 2 * g.px0, NT);
       }
     }
     if (t < 128) {
       // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
-      const int pl = t >> 6, rem = t & 63, r = rem >> 2, c = rem & 3;
+      const int pl = __builtin_amdgcn_readfirstlane(t >> 6), rem = t & 63, r = rem >> 2, c = rem & 3;
       if (g.cy0 + r < F.ch) {
         const float4* src = reinterpret_cast<const float4*>(csum[pl] + r * CBW + 8 * c);
         const float4 v0 = src[0], v1 = src[1];
@@ -695,17 +725,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 #pragma unroll
         for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
         const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
-        const int off = (g.cy0 + r) * (int)F.out_ls[1 + pl];
+        const int so = g.cy0 * (int)F.out_ls[1 + pl];
         if (F.out8)
           __builtin_amdgcn_raw_buffer_store_b64(
               __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
                                                  code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
-              oc_, off + g.cx0 + 8 * c, 0, NT);
+              oc_, lofs.sc, so + g.cx0, NT);
         else
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
                                                  code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
-              oc_, off + 2 * (g.cx0 + 8 * c), 0, NT);
+              oc_, lofs.sc, so + 2 * g.cx0, NT);
       }
     }
     if (!more) break;

@@ -1,0 +1,168 @@
+"""A second, independent restatement of the CPU chain, in float64 numpy,
+checked against the C oracle (oracle/h2s_oracle.c) on whole small frames.
+
+Test infrastructure only, like the oracle.  It is written from the stage
+definitions of SURVEY.md §8(a) T1-T10, not from the C code's structure:
+  * S1 (zscale t=linear:npl=100, src/utils.py:39): limited-range BT.2020-NCL
+    Y'CbCr, chroma bilinear (left-sited horizontally, centre-sited
+    vertically, zimg edge rule), ST 2084 EOTF x 10000/npl, or HLG inverse OETF +
+    OOTF (gamma 1.2, BT.2100 luma) x 1000/npl;
+  * S2 (tonemap=, vf_tonemap): desat 2 on the r+g+b luma, sig = max(R,G,B),
+    Reinhard / Hable / Mobius with their defaults, peak 10;
+  * S3 (zscale t=bt709): max(x, 0)^(1/2.4);
+  * S4 (lut3d interp=tetrahedral, src/utils.py:40): the tetrahedron of the
+    sorted fractions (a formulation without the six-way case split);
+  * S6 (swscale to yuv420p): BT.709 limited range, 2x2 chroma mean, round;
+  * S7 (eq=gamma, src/utils.py:41): vf_eq's 256-entry table;
+  * S8 (-pix_fmt, src/ffmpeg_command.py:355-360): the 8-bit code shifted.
+Measured: the two agree exactly on 11 of the 15 frames here, and the
+remaining frames differ in at most 2 samples per plane (float32 vs float64
+rounding); nearest-neighbour chroma, a one-pixel siting shift or peak 9
+instead of 10 each change 270-5000 samples of the same frame.  Contents
+with super-white codes (the 'edges' kind) are left out: there the C
+oracle follows vf_tonemap's float32 overflow (inf/NaN then lut3d's
+sanitising), which a float64 statement does not reproduce.  Two restatements
+in different precisions and formulations agreeing this closely is what this pins: it catches
+indexing, siting and stage-order errors in the C oracle, which the GPU
+parity tests would otherwise inherit.  It does not pin either against
+ffmpeg (parity unpinned)."""
+import numpy as np
+import pytest
+
+import hdr2sdr
+import oracle
+from hdr2sdr.synth import synth_frames
+
+TM = {'reinhard': 4, 'hable': 5, 'mobius': 6}
+LAT = {}
+
+
+def lattice(n):
+    if n not in LAT:
+        LAT[n] = hdr2sdr.generate_lattice(n).astype(np.float64).reshape(n, n, n, 3)  # [b][g][r]
+    return LAT[n]
+
+
+def upsample(c):
+    """4:2:0 plane (ch, cw) -> (2ch, 2cw): horizontal left-sited bilinear,
+    vertical centre-sited (1/4, 3/4); index -1 mirrors to 1, n clamps to n-1."""
+    ch, cw = c.shape
+    k = np.arange(cw)
+    nxt = np.minimum(k + 1, cw - 1)
+    h = np.empty((ch, 2 * cw))
+    h[:, 0::2] = c
+    h[:, 1::2] = 0.5 * c + 0.5 * c[:, nxt]
+    m = np.arange(ch)
+    up = np.abs(m - 1)                      # -1 -> 1
+    dn = np.minimum(m + 1, ch - 1)
+    v = np.empty((2 * ch, 2 * cw))
+    v[0::2] = 0.25 * h[up] + 0.75 * h
+    v[1::2] = 0.75 * h + 0.25 * h[dn]
+    return v
+
+
+def pq_eotf(e):
+    m1, m2, c1, c2, c3 = 2610 / 16384, 2523 / 4096 * 128, 3424 / 4096, 2413 / 4096 * 32, 2392 / 4096 * 32
+    xp = np.power(np.maximum(e, 0.0), 1.0 / m2)
+    y = np.power(np.maximum(xp - c1, 0.0) / np.maximum(c2 - c3 * xp, np.finfo(np.float32).tiny), 1.0 / m1)
+    return np.where(e > 0, y, 0.0)
+
+
+def hlg_inv(e):
+    a, b, c = 0.17883277, 0.28466892, 0.55991073
+    x = np.maximum(e, 0.0)
+    return np.where(x <= 0.5, x * x / 3.0, (np.exp((x - c) / a) + b) / 12.0)
+
+
+def curve(tm, x, peak=10.0):
+    if tm == 'reinhard':                     # tm_param unset: offset 1
+        return x / (x + 1.0) * (peak + 1.0) / peak
+    if tm == 'hable':
+        def h(v):
+            return (v * (v * 0.15 + 0.05) + 0.004) / (v * (v * 0.15 + 0.5) + 0.06) - 0.02 / 0.3
+        return h(x) / h(peak)
+    j = 0.3                                   # mobius
+    a = -j * j * (peak - 1.0) / (j * j - 2.0 * j + peak)
+    b = (j * j - 2.0 * j * peak + peak) / max(peak - 1.0, 1e-6)
+    return np.where(x <= j, x, (b * b + 2.0 * b * j + j * j) / (b - a) * (x + a) / (x + b))
+
+
+def tetrahedral(lat, s):
+    """lut3d tetrahedral at lattice coordinates s (..., 3) in [0, N-1]: walk
+    from the cell's low corner along the axes in decreasing fraction order."""
+    n = lat.shape[0]
+    base = np.minimum(np.floor(s), n - 2).astype(np.int64)
+    d = s - base
+    order = np.argsort(-d, axis=-1, kind='stable')
+    ds = np.take_along_axis(d, order, axis=-1)
+    w = np.stack([1.0 - ds[..., 0], ds[..., 0] - ds[..., 1], ds[..., 1] - ds[..., 2], ds[..., 2]], -1)
+    out = np.zeros(s.shape)
+    idx = base.copy()
+    for k in range(4):
+        if k:
+            step = np.zeros_like(idx)
+            np.put_along_axis(step, order[..., k - 1:k], 1, axis=-1)
+            idx = idx + step
+        out += w[..., k:k + 1] * lat[idx[..., 2], idx[..., 1], idx[..., 0]]
+    return out
+
+
+def eq_table(gamma):
+    v = np.arange(256) / 255.0
+    t = np.where(v <= 0, 0.0, np.power(np.maximum(v, 1e-300), 1.0 / gamma))
+    return np.where(t >= 1.0, 255, np.floor(256.0 * t)).astype(np.int64)
+
+
+def chain(y, u, v, bits_in, bits_out, hlg, tm, gamma, lut_n):
+    """One frame (planes as integer arrays) -> output planes."""
+    s = 1 << (bits_in - 8)
+    Y = (y.astype(np.float64) - 16 * s) / (219 * s)
+    Cb = upsample((u.astype(np.float64) - 128 * s) / (224 * s))
+    Cr = upsample((v.astype(np.float64) - 128 * s) / (224 * s))
+    kr, kb = 0.2627, 0.0593
+    kg = 1.0 - kr - kb
+    E = np.stack([Y + 2 * (1 - kr) * Cr, Y - 2 * kb * (1 - kb) / kg * Cb - 2 * kr * (1 - kr) / kg * Cr,
+                  Y + 2 * (1 - kb) * Cb], -1)
+    if hlg:
+        L = hlg_inv(E)
+        ys = L @ np.array([0.2627, 0.6780, 0.0593])
+        L = L * (np.where(ys > 0, np.power(np.maximum(ys, 0.0), 0.2), 0.0) * 10.0)[..., None]
+    else:
+        L = pq_eotf(E) * 100.0
+    luma = L.sum(-1)
+    ob = np.maximum(luma - 2.0, 1e-6) / np.maximum(luma, 1e-6)
+    L = L * (1 - ob)[..., None] + (luma * ob)[..., None]
+    sig = np.maximum(L.max(-1), 1e-6)
+    L = L * (curve(tm, sig) / sig)[..., None]
+    G = np.power(np.maximum(L, 0.0), 1.0 / 2.4)
+    rgb = np.clip(tetrahedral(lattice(lut_n), np.clip(G * (lut_n - 1), 0, lut_n - 1)), 0.0, 1.0)
+    Yo = rgb @ np.array([0.2126, 0.7152, 0.0722])
+    cb = (rgb[..., 2] - Yo) / 1.8556
+    cr = (rgb[..., 0] - Yo) / 1.5748
+    yq = np.clip(np.floor(16.0 + 219.0 * Yo + 0.5), 0, 255).astype(np.int64)
+    quad = lambda p: (p[0::2, 0::2] + p[0::2, 1::2] + p[1::2, 0::2] + p[1::2, 1::2]) / 4.0
+    cq = [np.clip(np.floor(128.0 + 224.0 * quad(p) + 0.5), 0, 255).astype(np.int64) for p in (cb, cr)]
+    sh = bits_out - 8
+    return eq_table(gamma)[yq] << sh, cq[0] << sh, cq[1] << sh
+
+
+CASES = [('hable', 10, 10, False, 2.2, 65), ('reinhard', 10, 8, False, 1.0, 33), ('mobius', 10, 10, False, 1.0, 65),
+         ('hable', 12, 12, True, 1.0, 65), ('reinhard', 12, 10, True, 1.6, 17)]
+
+
+@pytest.mark.parametrize('kind', ['smooth', 'ramp', 'uniform'])
+@pytest.mark.parametrize('tm,bits_in,bits_out,hlg,gamma,lut_n', CASES)
+def test_independent_restatement_matches_oracle(kind, tm, bits_in, bits_out, hlg, gamma, lut_n):
+    W, H = 96, 64
+    fb = synth_frames(kind, 1, W, H, bits_in, device='cpu', seed=11).to_numpy()
+    p = oracle.default_params(tonemap=TM[tm], bits_in=bits_in, bits_out=bits_out, transfer_in=1 if hlg else 0,
+                              gamma=gamma)
+    got = hdr2sdr.FrameBatch(oracle.process(p, hdr2sdr.generate_lattice(lut_n), fb.buf, W, H), W, H, bits_out)
+    want = chain(fb.y[0], fb.u[0], fb.v[0], bits_in, bits_out, hlg, tm, gamma, lut_n)
+    step = 1 << (bits_out - 8)
+    for name, a, b in zip('YUV', (got.y[0], got.u[0], got.v[0]), want):
+        d = np.abs(a.astype(np.int64) - b)
+        # eq amplifies a luma flip by the table's slope (<= 256/255 * (1/g) * v^(1/g - 1) steps near black)
+        bound = step * (1 if name != 'Y' or gamma == 1.0 else 3)
+        assert d.max() <= bound, (name, int(d.max()))
+        assert (d > 0).mean() <= 5e-3, (name, float((d > 0).mean()))
