@@ -15,9 +15,10 @@ definitions of SURVEY.md §8(a) T1-T10, not from the C code's structure:
   * S6 (swscale to yuv420p): BT.709 limited range, 2x2 chroma mean, round;
   * S7 (eq=gamma, src/utils.py:41): vf_eq's 256-entry table;
   * S8 (-pix_fmt, src/ffmpeg_command.py:355-360): the 8-bit code shifted.
-Measured: the two agree exactly on 11 of the 15 frames here, and the
-remaining frames differ in at most 2 samples per plane (float32 vs float64
-rounding); nearest-neighbour chroma, a one-pixel siting shift or peak 9
+Also the native quantiser, the LUT off (legacy closed form, its matrix
+derived here from the primaries) and the weighted desat luma.  Measured: the
+two agree exactly on 14 of the 27 frames here, and the others differ in at
+most 5 of 6144 samples per plane, by one step (float32 vs float64 rounding); nearest-neighbour chroma, a one-pixel siting shift or peak 9
 instead of 10 each change 270-5000 samples of the same frame.  Contents
 with super-white codes (the 'edges' kind) are left out: there the C
 oracle follows vf_tonemap's float32 overflow (inf/NaN then lut3d's
@@ -107,14 +108,32 @@ def tetrahedral(lat, s):
     return out
 
 
-def eq_table(gamma):
-    v = np.arange(256) / 255.0
+def eq_table(gamma, q=8):
+    qmax = (1 << q) - 1
+    v = np.arange(qmax + 1) / qmax
     t = np.where(v <= 0, 0.0, np.power(np.maximum(v, 1e-300), 1.0 / gamma))
-    return np.where(t >= 1.0, 255, np.floor(256.0 * t)).astype(np.int64)
+    return np.where(t >= 1.0, qmax, np.floor((qmax + 1) * t)).astype(np.int64)
 
 
-def chain(y, u, v, bits_in, bits_out, hlg, tm, gamma, lut_n):
-    """One frame (planes as integer arrays) -> output planes."""
+def rgb_to_xyz(prim, white=(0.3127, 0.3290)):
+    """RGB -> XYZ from the primaries' and white's xy chromaticities"""
+    P = np.array([[x / y, 1.0, (1 - x - y) / y] for x, y in prim]).T
+    wx, wy = white
+    Wv = np.array([wx / wy, 1.0, (1 - wx - wy) / wy])
+    return P * np.linalg.solve(P, Wv)
+
+
+def m2020_709():
+    """linear BT.2020 -> BT.709 (the LUT-off legacy gamut step, zscale p=bt709)"""
+    m2020 = rgb_to_xyz([(0.708, 0.292), (0.170, 0.797), (0.131, 0.046)])
+    m709 = rgb_to_xyz([(0.64, 0.33), (0.30, 0.60), (0.15, 0.06)])
+    return np.linalg.solve(m709, m2020)
+
+
+def chain(y, u, v, bits_in, bits_out, hlg, tm, gamma, lut_n, native=False, luma_w=(1.0, 1.0, 1.0)):
+    """One frame (planes as integer arrays) -> output planes.  lut_n = 0: the
+    LUT off (linear BT.2020 -> BT.709 matrix, BT.1886 encode, clip); native:
+    quantise at the output depth (compat8 quantises at 8 bits, then shifts)."""
     s = 1 << (bits_in - 8)
     Y = (y.astype(np.float64) - 16 * s) / (219 * s)
     Cb = upsample((u.astype(np.float64) - 128 * s) / (224 * s))
@@ -129,37 +148,50 @@ def chain(y, u, v, bits_in, bits_out, hlg, tm, gamma, lut_n):
         L = L * (np.where(ys > 0, np.power(np.maximum(ys, 0.0), 0.2), 0.0) * 10.0)[..., None]
     else:
         L = pq_eotf(E) * 100.0
-    luma = L.sum(-1)
+    luma = L @ np.array(luma_w)
     ob = np.maximum(luma - 2.0, 1e-6) / np.maximum(luma, 1e-6)
     L = L * (1 - ob)[..., None] + (luma * ob)[..., None]
     sig = np.maximum(L.max(-1), 1e-6)
     L = L * (curve(tm, sig) / sig)[..., None]
-    G = np.power(np.maximum(L, 0.0), 1.0 / 2.4)
-    rgb = np.clip(tetrahedral(lattice(lut_n), np.clip(G * (lut_n - 1), 0, lut_n - 1)), 0.0, 1.0)
+    if lut_n:
+        G = np.power(np.maximum(L, 0.0), 1.0 / 2.4)
+        rgb = np.clip(tetrahedral(lattice(lut_n), np.clip(G * (lut_n - 1), 0, lut_n - 1)), 0.0, 1.0)
+    else:
+        rgb = np.clip(np.power(np.maximum(L @ m2020_709().T, 0.0), 1.0 / 2.4), 0.0, 1.0)
     Yo = rgb @ np.array([0.2126, 0.7152, 0.0722])
     cb = (rgb[..., 2] - Yo) / 1.8556
     cr = (rgb[..., 0] - Yo) / 1.5748
-    yq = np.clip(np.floor(16.0 + 219.0 * Yo + 0.5), 0, 255).astype(np.int64)
+    q = bits_out if native else 8
+    qs, qmax = float(1 << (q - 8)), (1 << q) - 1
+    yq = np.clip(np.floor((16.0 + 219.0 * Yo) * qs + 0.5), 0, qmax).astype(np.int64)
     quad = lambda p: (p[0::2, 0::2] + p[0::2, 1::2] + p[1::2, 0::2] + p[1::2, 1::2]) / 4.0
-    cq = [np.clip(np.floor(128.0 + 224.0 * quad(p) + 0.5), 0, 255).astype(np.int64) for p in (cb, cr)]
-    sh = bits_out - 8
-    return eq_table(gamma)[yq] << sh, cq[0] << sh, cq[1] << sh
+    cq = [np.clip(np.floor((128.0 + 224.0 * quad(p)) * qs + 0.5), 0, qmax).astype(np.int64) for p in (cb, cr)]
+    sh = bits_out - q
+    return eq_table(gamma, q)[yq] << sh, cq[0] << sh, cq[1] << sh
 
 
 CASES = [('hable', 10, 10, False, 2.2, 65), ('reinhard', 10, 8, False, 1.0, 33), ('mobius', 10, 10, False, 1.0, 65),
-         ('hable', 12, 12, True, 1.0, 65), ('reinhard', 12, 10, True, 1.6, 17)]
+         ('hable', 12, 12, True, 1.0, 65), ('reinhard', 12, 10, True, 1.6, 17),
+         # native quantiser, LUT off (legacy closed form), weighted desat luma (App. B.1 switch)
+         ('hable', 10, 10, False, 1.0, 65, 'native'), ('hable', 12, 12, True, 2.2, 65, 'native'),
+         ('mobius', 10, 10, False, 2.2, 0), ('hable', 10, 10, False, 1.0, 65, 'bt2020')]
 
 
 @pytest.mark.parametrize('kind', ['smooth', 'ramp', 'uniform'])
-@pytest.mark.parametrize('tm,bits_in,bits_out,hlg,gamma,lut_n', CASES)
-def test_independent_restatement_matches_oracle(kind, tm, bits_in, bits_out, hlg, gamma, lut_n):
+@pytest.mark.parametrize('case', CASES, ids=lambda c: '-'.join(map(str, c)))
+def test_independent_restatement_matches_oracle(kind, case):
+    tm, bits_in, bits_out, hlg, gamma, lut_n = case[:6]
+    native, weighted = 'native' in case[6:], 'bt2020' in case[6:]
     W, H = 96, 64
     fb = synth_frames(kind, 1, W, H, bits_in, device='cpu', seed=11).to_numpy()
     p = oracle.default_params(tonemap=TM[tm], bits_in=bits_in, bits_out=bits_out, transfer_in=1 if hlg else 0,
-                              gamma=gamma)
-    got = hdr2sdr.FrameBatch(oracle.process(p, hdr2sdr.generate_lattice(lut_n), fb.buf, W, H), W, H, bits_out)
-    want = chain(fb.y[0], fb.u[0], fb.v[0], bits_in, bits_out, hlg, tm, gamma, lut_n)
-    step = 1 << (bits_out - 8)
+                              gamma=gamma, mode=1 if native else 0, lut_enabled=1 if lut_n else 0,
+                              desat_luma=1 if weighted else 0)
+    lat = hdr2sdr.generate_lattice(lut_n) if lut_n else None
+    got = hdr2sdr.FrameBatch(oracle.process(p, lat, fb.buf, W, H), W, H, bits_out)
+    want = chain(fb.y[0], fb.u[0], fb.v[0], bits_in, bits_out, hlg, tm, gamma, lut_n, native=native,
+                 luma_w=(0.2627, 0.6780, 0.0593) if weighted else (1.0, 1.0, 1.0))
+    step = 1 << (bits_out - (bits_out if native else 8))
     for name, a, b in zip('YUV', (got.y[0], got.u[0], got.v[0]), want):
         d = np.abs(a.astype(np.int64) - b)
         # eq amplifies a luma flip by the table's slope (<= 256/255 * (1/g) * v^(1/g - 1) steps near black)
