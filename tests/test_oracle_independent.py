@@ -19,7 +19,12 @@ Also the native quantiser, the LUT off (legacy closed form, its matrix
 derived here from the primaries) and the weighted desat luma.  Measured: the
 two agree exactly on 14 of the 27 frames here, and the others differ in at
 most 5 of 6144 samples per plane, by one step (float32 vs float64 rounding); nearest-neighbour chroma, a one-pixel siting shift or peak 9
-instead of 10 each change 270-5000 samples of the same frame.  Contents
+instead of 10 each change 270-5000 samples of the same frame.  The
+libplacebo branch (C3's structure with BT.2390 as the max(R,G,B) gain:
+BT.1886 encode against the target black, rgba8 download, lut3d's truncating
+8-bit path, Y'CbCr at the output depth) agrees to <= 10 of 6144 samples per
+plane, within the lattice's step for an rgba8 code rounded the other way;
+knee offset 0.5 or a 100-nit white instead changes 1000-4600 samples.  Contents
 with super-white codes (the 'edges' kind) are left out: there the C
 oracle follows vf_tonemap's float32 overflow (inf/NaN then lut3d's
 sanitising), which a float64 statement does not reproduce.  Two restatements
@@ -198,3 +203,79 @@ def test_independent_restatement_matches_oracle(kind, case):
         bound = step * (1 if name != 'Y' or gamma == 1.0 else 3)
         assert d.max() <= bound, (name, int(d.max()))
         assert (d > 0).mean() <= 5e-3, (name, float((d > 0).mean()))
+
+
+# ---- the libplacebo branch (C3, src/utils.py:444-460), max(R,G,B) form ----
+def pq_encode(y):
+    """ST 2084 inverse EOTF, y = luminance / 10000"""
+    m1, m2, c1, c2, c3 = 2610 / 16384, 2523 / 4096 * 128, 3424 / 4096, 2413 / 4096 * 32, 2392 / 4096 * 32
+    ym = np.power(np.maximum(y, 0.0), m1)
+    return np.power((c1 + c2 * ym) / (1.0 + c3 * ym), m2)
+
+
+def bt2390(e1, peak_nits=1000.0, white=203.0, knee_offset=1.0):
+    """libplacebo bt2390 (PQ in, PQ out) against the SDR target [white/1000,
+    white]: Hermite knee at ks = (1 + k) maxLum - k, then the black-point
+    lift x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum"""
+    lo, hi = pq_encode(0.0), pq_encode(peak_nits / 1e4)
+    ml = (pq_encode(white / 1e4) - lo) / (hi - lo)
+    mn = (pq_encode(white / 1000.0 / 1e4) - lo) / (hi - lo)
+    ks = (1.0 + knee_offset) * ml - knee_offset
+    x = np.clip((e1 - lo) / (hi - lo), 0.0, 1.0)
+    t = (x - ks) / (1.0 - ks)
+    herm = (2 * t ** 3 - 3 * t ** 2 + 1) * ks + (t ** 3 - 2 * t ** 2 + t) * (1 - ks) + (-2 * t ** 3 + 3 * t ** 2) * ml
+    x = np.where(x > ks, herm, x)
+    bp = min(1.0 / mn, 4.0)
+    gain = 1.0 / (1.0 + mn / ml * (1.0 - ml) ** bp)
+    x = np.where(x < 1.0, gain * (x + mn * np.power(np.maximum(1.0 - x, 0.0), bp) - mn) + mn, x)
+    return x * (hi - lo) + lo
+
+
+def chain_lp(y, u, v, bits_out, lut_n, white=203.0):
+    """PQ 10-bit in; tone curve on max(R,G,B); BT.1886 encode against the
+    target black; 8-bit rgba download; lut3d's 8-bit path (truncating);
+    BT.709 limited-range Y'CbCr at the output depth, no eq (gamma 1)"""
+    s = 4
+    Y = (y.astype(np.float64) - 16 * s) / (219 * s)
+    Cb = upsample((u.astype(np.float64) - 128 * s) / (224 * s))
+    Cr = upsample((v.astype(np.float64) - 128 * s) / (224 * s))
+    kr, kb = 0.2627, 0.0593
+    kg = 1.0 - kr - kb
+    E = np.stack([Y + 2 * (1 - kr) * Cr, Y - 2 * kb * (1 - kb) / kg * Cb - 2 * kr * (1 - kr) / kg * Cr,
+                  Y + 2 * (1 - kb) * Cb], -1)
+    L = pq_eotf(E) * 1e4                                     # nits
+    sig = np.maximum(L.max(-1), 1e-4)                        # (1e-6 of npl = 100 nits)
+    out = pq_eotf(bt2390(pq_encode(sig / 1e4))) * 1e4 / white
+    T = L * (out / sig)[..., None]                           # units of the SDR white
+    lb = (1.0 / 1000.0) ** (1 / 2.4)
+    enc = np.power(np.maximum(T, 0.0) / (1 - lb) ** 2.4, 1 / 2.4) - lb / (1 - lb)
+    q8 = np.floor(np.clip(enc, 0.0, 1.0) * 255.0 + 0.5)
+    o = tetrahedral(lattice(lut_n), q8 / 255.0 * (lut_n - 1))
+    rgb = np.clip(np.floor(o * 255.0), 0, 255) / 255.0
+    Yo = rgb @ np.array([0.2126, 0.7152, 0.0722])
+    cb = (rgb[..., 2] - Yo) / 1.8556
+    cr = (rgb[..., 0] - Yo) / 1.5748
+    qs, qmax = float(1 << (bits_out - 8)), (1 << bits_out) - 1
+    yq = np.clip(np.floor((16.0 + 219.0 * Yo) * qs + 0.5), 0, qmax).astype(np.int64)
+    quad = lambda p: (p[0::2, 0::2] + p[0::2, 1::2] + p[1::2, 0::2] + p[1::2, 1::2]) / 4.0
+    cq = [np.clip(np.floor((128.0 + 224.0 * quad(p)) * qs + 0.5), 0, qmax).astype(np.int64) for p in (cb, cr)]
+    return yq, cq[0], cq[1]
+
+
+@pytest.mark.parametrize('kind', ['smooth', 'ramp', 'uniform'])
+@pytest.mark.parametrize('bits_out,lut_n', [(10, 65), (8, 33)])
+def test_independent_libplacebo_branch_matches_oracle(kind, bits_out, lut_n):
+    """C3's structure (rgba8 download -> lut3d 8-bit -> Y'CbCr at depth) with
+    BT.2390 as the max(R,G,B) gain.  An rgba8 code that rounds the other way
+    moves the truncated LUT output by a few 8-bit steps, so a sample may differ
+    by up to the lattice's steepest step, and only rarely."""
+    W, H = 96, 64
+    fb = synth_frames(kind, 1, W, H, 10, device='cpu', seed=13).to_numpy()
+    p = oracle.default_params(tonemap=7, bits_out=bits_out, pipeline=2, lp_tone=1)
+    got = hdr2sdr.FrameBatch(oracle.process(p, hdr2sdr.generate_lattice(lut_n), fb.buf, W, H), W, H, bits_out)
+    want = chain_lp(fb.y[0], fb.u[0], fb.v[0], bits_out, lut_n)
+    k8 = 1 << (bits_out - 8)
+    for name, a, b in zip('YUV', (got.y[0], got.u[0], got.v[0]), want):
+        d = np.abs(a.astype(np.int64) - b)
+        assert d.max() <= 8 * k8, (name, int(d.max()))
+        assert (d > 0).mean() <= 1e-2, (name, float((d > 0).mean()))
