@@ -20,7 +20,8 @@ derived here from the primaries) and the weighted desat luma.  Measured: the
 two agree exactly on 14 of the 27 frames here, and the others differ in at
 most 5 of 6144 samples per plane, by one step (float32 vs float64 rounding); nearest-neighbour chroma, a one-pixel siting shift or peak 9
 instead of 10 each change 270-5000 samples of the same frame.  The
-libplacebo branch (C3's structure with BT.2390 as the max(R,G,B) gain:
+libplacebo branch (C3's structure with BT.2390 as the max(R,G,B) gain or on
+the IPT-PQ intensity, matrices derived here from the primaries and HPE rows:
 BT.1886 encode against the target black, rgba8 download, lut3d's truncating
 8-bit path, Y'CbCr at the output depth) agrees to <= 10 of 6144 samples per
 plane, within the lattice's step for an rgba8 code rounded the other way;
@@ -231,8 +232,15 @@ def bt2390(e1, peak_nits=1000.0, white=203.0, knee_offset=1.0):
     return x * (hi - lo) + lo
 
 
-def chain_lp(y, u, v, bits_out, lut_n, white=203.0):
-    """PQ 10-bit in; tone curve on max(R,G,B); BT.1886 encode against the
+def rgb_to_lms():
+    """linear BT.2020 -> LMS (Hunt-Pointer-Estevez rows of XYZ, D65 white)"""
+    hpe = np.array([[0.4002, 0.7076, -0.0808], [-0.2263, 1.1653, 0.0457], [0.0, 0.0, 0.9182]])
+    return hpe @ rgb_to_xyz([(0.708, 0.292), (0.170, 0.797), (0.131, 0.046)])
+
+
+def chain_lp(y, u, v, bits_out, lut_n, white=203.0, ipt=False):
+    """PQ 10-bit in; tone curve on max(R,G,B) (or on the intensity of IPT-PQ,
+    P and T kept: L'M'S' += I' - I); BT.1886 encode against the
     target black; 8-bit rgba download; lut3d's 8-bit path (truncating);
     BT.709 limited-range Y'CbCr at the output depth, no eq (gamma 1)"""
     s = 4
@@ -244,9 +252,16 @@ def chain_lp(y, u, v, bits_out, lut_n, white=203.0):
     E = np.stack([Y + 2 * (1 - kr) * Cr, Y - 2 * kb * (1 - kb) / kg * Cb - 2 * kr * (1 - kr) / kg * Cr,
                   Y + 2 * (1 - kb) * Cb], -1)
     L = pq_eotf(E) * 1e4                                     # nits
-    sig = np.maximum(L.max(-1), 1e-4)                        # (1e-6 of npl = 100 nits)
-    out = pq_eotf(bt2390(pq_encode(sig / 1e4))) * 1e4 / white
-    T = L * (out / sig)[..., None]                           # units of the SDR white
+    if ipt:
+        r2l = rgb_to_lms()
+        q = pq_encode(np.minimum(L, 1e8) / 1e4 @ r2l.T)
+        I = q @ np.array([0.4, 0.4, 0.2])
+        lms = pq_eotf(q + (bt2390(I) - I)[..., None])
+        T = lms @ np.linalg.inv(r2l).T * (1e4 / white)
+    else:
+        sig = np.maximum(L.max(-1), 1e-4)                    # (1e-6 of npl = 100 nits)
+        out = pq_eotf(bt2390(pq_encode(sig / 1e4))) * 1e4 / white
+        T = L * (out / sig)[..., None]                       # units of the SDR white
     lb = (1.0 / 1000.0) ** (1 / 2.4)
     enc = np.power(np.maximum(T, 0.0) / (1 - lb) ** 2.4, 1 / 2.4) - lb / (1 - lb)
     q8 = np.floor(np.clip(enc, 0.0, 1.0) * 255.0 + 0.5)
@@ -264,16 +279,17 @@ def chain_lp(y, u, v, bits_out, lut_n, white=203.0):
 
 @pytest.mark.parametrize('kind', ['smooth', 'ramp', 'uniform'])
 @pytest.mark.parametrize('bits_out,lut_n', [(10, 65), (8, 33)])
-def test_independent_libplacebo_branch_matches_oracle(kind, bits_out, lut_n):
+@pytest.mark.parametrize('form', ['max-rgb', 'ipt'])
+def test_independent_libplacebo_branch_matches_oracle(kind, bits_out, lut_n, form):
     """C3's structure (rgba8 download -> lut3d 8-bit -> Y'CbCr at depth) with
-    BT.2390 as the max(R,G,B) gain.  An rgba8 code that rounds the other way
+    BT.2390 as the max(R,G,B) gain or on the IPT-PQ intensity.  An rgba8 code that rounds the other way
     moves the truncated LUT output by a few 8-bit steps, so a sample may differ
     by up to the lattice's steepest step, and only rarely."""
     W, H = 96, 64
     fb = synth_frames(kind, 1, W, H, 10, device='cpu', seed=13).to_numpy()
-    p = oracle.default_params(tonemap=7, bits_out=bits_out, pipeline=2, lp_tone=1)
+    p = oracle.default_params(tonemap=7, bits_out=bits_out, pipeline=2, lp_tone=1 if form == 'max-rgb' else 0)
     got = hdr2sdr.FrameBatch(oracle.process(p, hdr2sdr.generate_lattice(lut_n), fb.buf, W, H), W, H, bits_out)
-    want = chain_lp(fb.y[0], fb.u[0], fb.v[0], bits_out, lut_n)
+    want = chain_lp(fb.y[0], fb.u[0], fb.v[0], bits_out, lut_n, ipt=form == 'ipt')
     k8 = 1 << (bits_out - 8)
     for name, a, b in zip('YUV', (got.y[0], got.u[0], got.v[0]), want):
         d = np.abs(a.astype(np.int64) - b)
