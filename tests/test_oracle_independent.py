@@ -238,12 +238,12 @@ def rgb_to_lms():
     return hpe @ rgb_to_xyz([(0.708, 0.292), (0.170, 0.797), (0.131, 0.046)])
 
 
-def chain_lp(y, u, v, bits_out, lut_n, white=203.0, ipt=False):
+def chain_lp(y, u, v, bits_out, lut_n, white=203.0, ipt=False, bits_in=10, hlg=False):
     """PQ 10-bit in; tone curve on max(R,G,B) (or on the intensity of IPT-PQ,
     P and T kept: L'M'S' += I' - I); BT.1886 encode against the
     target black; 8-bit rgba download; lut3d's 8-bit path (truncating);
     BT.709 limited-range Y'CbCr at the output depth, no eq (gamma 1)"""
-    s = 4
+    s = 1 << (bits_in - 8)
     Y = (y.astype(np.float64) - 16 * s) / (219 * s)
     Cb = upsample((u.astype(np.float64) - 128 * s) / (224 * s))
     Cr = upsample((v.astype(np.float64) - 128 * s) / (224 * s))
@@ -251,7 +251,12 @@ def chain_lp(y, u, v, bits_out, lut_n, white=203.0, ipt=False):
     kg = 1.0 - kr - kb
     E = np.stack([Y + 2 * (1 - kr) * Cr, Y - 2 * kb * (1 - kb) / kg * Cb - 2 * kr * (1 - kr) / kg * Cr,
                   Y + 2 * (1 - kb) * Cb], -1)
-    L = pq_eotf(E) * 1e4                                     # nits
+    if hlg:                                                  # 1000-nit HLG display (OOTF gamma 1.2)
+        L = hlg_inv(E)
+        ys = L @ np.array([0.2627, 0.6780, 0.0593])
+        L = L * (np.where(ys > 0, np.power(np.maximum(ys, 0.0), 0.2), 0.0) * 1000.0)[..., None]
+    else:
+        L = pq_eotf(E) * 1e4                                 # nits
     if ipt:
         r2l = rgb_to_lms()
         q = pq_encode(np.minimum(L, 1e8) / 1e4 @ r2l.T)
@@ -278,18 +283,20 @@ def chain_lp(y, u, v, bits_out, lut_n, white=203.0, ipt=False):
 
 
 @pytest.mark.parametrize('kind', ['smooth', 'ramp', 'uniform'])
-@pytest.mark.parametrize('bits_out,lut_n', [(10, 65), (8, 33)])
+@pytest.mark.parametrize('bits_in,bits_out,lut_n', [(10, 10, 65), (10, 8, 33), (12, 12, 65)])
 @pytest.mark.parametrize('form', ['max-rgb', 'ipt'])
-def test_independent_libplacebo_branch_matches_oracle(kind, bits_out, lut_n, form):
+def test_independent_libplacebo_branch_matches_oracle(kind, bits_in, bits_out, lut_n, form):
     """C3's structure (rgba8 download -> lut3d 8-bit -> Y'CbCr at depth) with
     BT.2390 as the max(R,G,B) gain or on the IPT-PQ intensity.  An rgba8 code that rounds the other way
     moves the truncated LUT output by a few 8-bit steps, so a sample may differ
     by up to the lattice's steepest step, and only rarely."""
     W, H = 96, 64
-    fb = synth_frames(kind, 1, W, H, 10, device='cpu', seed=13).to_numpy()
-    p = oracle.default_params(tonemap=7, bits_out=bits_out, pipeline=2, lp_tone=1 if form == 'max-rgb' else 0)
+    hlg = bits_in == 12                      # HLG 12-bit input through the same branch
+    fb = synth_frames(kind, 1, W, H, bits_in, device='cpu', seed=13).to_numpy()
+    p = oracle.default_params(tonemap=7, bits_in=bits_in, bits_out=bits_out, transfer_in=1 if hlg else 0, pipeline=2,
+                              lp_tone=1 if form == 'max-rgb' else 0)
     got = hdr2sdr.FrameBatch(oracle.process(p, hdr2sdr.generate_lattice(lut_n), fb.buf, W, H), W, H, bits_out)
-    want = chain_lp(fb.y[0], fb.u[0], fb.v[0], bits_out, lut_n, ipt=form == 'ipt')
+    want = chain_lp(fb.y[0], fb.u[0], fb.v[0], bits_out, lut_n, ipt=form == 'ipt', bits_in=bits_in, hlg=hlg)
     k8 = 1 << (bits_out - 8)
     for name, a, b in zip('YUV', (got.y[0], got.u[0], got.v[0]), want):
         d = np.abs(a.astype(np.int64) - b)
