@@ -602,3 +602,43 @@ def test_peak_exchange_and_lp_tone_errors(tm):
     c.lp_tone = 7
     assert tm._L.h2s_set_params(tm._ctx, ctypes.byref(c)) == _abi.H2S_E_INVALID_ARG
     tm.set_params(params)
+
+
+@pytest.mark.parametrize('W,H', [(130, 98), (194, 66)])
+@pytest.mark.parametrize('tmname', ['hable', 'bt.2390'])
+def test_tile_interior_boundaries(tm, W, H, tmname):
+    """k_tile addresses a tile from launch-constant lane offsets when its rows
+    and its chroma halo lie inside the frame (cy0 >= 1, cy0 + 17 <= ch,
+    cx0 + 33 <= cw) and clamps per lane otherwise.  These sizes put tiles
+    exactly on each equality (cw = 32k + 1, ch = 16m + 1); rows padded to 16
+    bytes send them through the tile kernel (+ k_process for the W % 64
+    columns).  Equal to the oracle, and to the tight layout's generic-kernel
+    result within the same bound."""
+    import ctypes
+    import torch
+    from hdr2sdr import _abi
+    F = 2
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, gamma=2.2 if tmname == 'hable' else 1.0)
+    got_tight, want, _ = run_both(tm, params, 'smooth', W, H, nframes=F)
+    src = synth_frames('smooth', F, W, H, 10, device='cpu', seed=11).to_numpy()
+    ls = [(W * 2 + 15) // 16 * 16, (W + 15) // 16 * 16, (W + 15) // 16 * 16]
+    fp = H * ls[0] + 2 * (H // 2) * ls[1]
+
+    def desc(buf):
+        d = _abi.H2SFrames()
+        base = buf.data_ptr()
+        d.data[0], d.data[1], d.data[2] = base, base + H * ls[0], base + H * ls[0] + H // 2 * ls[1]
+        for p in range(3):
+            d.linesize[p], d.frame_pitch[p] = ls[p], fp
+        d.width, d.height, d.bits, d.location = W, H, 10, _abi.LOC_DEVICE
+        return d
+
+    raw_in = torch.from_numpy(_pack_padded(src.buf, W, H, 10, ls, fp)).cuda()
+    raw_out = torch.zeros(F * fp + 64, dtype=torch.uint8, device='cuda')
+    di, do = desc(raw_in), desc(raw_out)
+    assert tm._L.h2s_query_path(tm._ctx, ctypes.byref(di), ctypes.byref(do)) == _abi.PATH_TILE_TAIL
+    tm._check(tm._L.h2s_process(tm._ctx, ctypes.byref(di), ctypes.byref(do), F, None))
+    torch.cuda.synchronize()
+    got = _unpack_padded(raw_out.cpu().numpy(), F, W, H, 10, ls, fp).astype(np.int64)
+    assert_close_int(params, got, want, W, H)
+    assert_close_int(params, got, got_tight, W, H)
