@@ -357,6 +357,8 @@ def main():
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
+            # the read-only share (the input bytes alone)
+            'read_only_frac': round(1.5 * sb_in * px_per_launch / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             'traffic': None,
             'kernel': 'k_tile (h2s_fast.hip)',
             'kernel_ms': round(kms, 4),
