@@ -203,11 +203,11 @@ def main():
     tm = hdr2sdr.Tonemapper(local, params, lattice_host)
     W, H, B = args.width, args.height, args.frames
 
-    def run(kind):
+    def run(kind, make_src=None):
         # this rank's frames: global indices [rank*B, rank*B + B) of a
         # world*B-frame sequence (shard_range), synthesised in place
         a, b = shard_range(world * B, world, rank)
-        src = synth_frames(kind, b - a, W, H, args.bits_in, device=dev, seed=0x5EED + a)
+        src = make_src(b - a) if make_src else synth_frames(kind, b - a, W, H, args.bits_in, device=dev, seed=0x5EED + a)
         dst = hdr2sdr.FrameBatch.empty_torch(b - a, W, H, args.bits_out, dev)
         stream = torch.cuda.current_stream(dev)
         for _ in range(args.warmup):
@@ -238,6 +238,19 @@ def main():
     if not args.no_alt:
         el_u, kms_u, px_u, _ = run('uniform')
         alt = {'kind': 'uniform', 'value': round(px_u / el_u / 1e6, 1), 'kernel_ms': round(kms_u, 4)}
+
+    # real content: the reference's own website HDR frame (a 4K capture of PQ
+    # BT.2020 R'G'B', tests/golden/website_hdr_full.npz), repeated per frame
+    real = None
+    real_npz = os.path.join(REPO, 'tests', 'golden', 'website_hdr_full.npz')
+    if world == 1 and not args.no_alt and os.path.exists(real_npz) and (W, H) == (3840, 2160):
+        import numpy as np
+        from hdr2sdr.synth import frames_from_rgb8
+        rgb8 = np.load(real_npz)['hdr']
+        el_r, kms_r, px_r, _ = run('real', lambda n: frames_from_rgb8(rgb8, n, args.bits_in, dev))
+        real = {'kind': 'website HDR frame (reference HDR to SDR Website/hdr-frame.png, PQ BT.2020 capture)',
+                'value': round(px_r / el_r / 1e6, 1), 'kernel_ms': round(kms_r, 4)}
+        del rgb8
 
     # PCIe-inclusive rate (host-resident, page-locked frames through the
     # h2s_process host path: H2D, kernel, D2H): what the drop-in planner's
@@ -348,6 +361,7 @@ def main():
             'parallelism': f'frame-sharded x{world} ({backend if world > 1 else "single rank"}; '
                            f'params + LUT broadcast only)',
             'alt_content': alt,
+            'real_content': real,
             'other_configs': other,
             'host_path': host_path,
         },

@@ -15,6 +15,10 @@ synthetic planar frames of the same shape:
 
 Generation runs in torch on whatever device the caller names, seeded per
 frame from ``seed + frame_index``.
+
+``frames_from_rgb8`` turns a captured frame (8-bit R'G'B' read as PQ BT.2020
+codes, e.g. the reference's own website HDR frame, tests/golden/) into the
+same planar layout: real content between ``smooth`` and ``uniform``.
 """
 from __future__ import annotations
 
@@ -102,4 +106,18 @@ def synth_frames(kind: str, nframes: int, width: int, height: int, bits: int = 1
         fb.y[i] = Y.to(fb.buf.dtype)
         fb.u[i] = U.to(fb.buf.dtype)
         fb.v[i] = V.to(fb.buf.dtype)
+    return fb
+
+
+def frames_from_rgb8(rgb8: Any, nframes: int, bits: int = 10, device: Any = 'cpu') -> FrameBatch:
+    """uint8 [H, W, 3] R'G'B' (PQ BT.2020 codes / 255) -> ``nframes`` copies
+    as BT.2020-NCL limited-range Y'CbCr 4:2:0 (H and W cropped to even)."""
+    import torch
+    t = torch.as_tensor(rgb8)
+    h, w = t.shape[0] & ~1, t.shape[1] & ~1
+    rgb = t[:h, :w].permute(2, 0, 1).to(device=device, dtype=torch.float32) / 255.0
+    Y, U, V = _rgb_to_frame(rgb, bits)
+    fb = FrameBatch.empty_torch(nframes, w, h, bits, device)
+    for i in range(nframes):
+        fb.y[i], fb.u[i], fb.v[i] = Y.to(fb.buf.dtype), U.to(fb.buf.dtype), V.to(fb.buf.dtype)
     return fb

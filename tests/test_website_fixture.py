@@ -205,3 +205,19 @@ def test_hip_preview_path_on_the_website_pair():
                                 fb.width, fb.height).astype(np.int32)
     assert (np.abs(got - want) <= 1).mean() > 0.99
     assert float(np.abs(got[::2, ::2] - sdr).mean()) < 3.3
+
+
+def test_full_website_frame_as_bench_input():
+    """bench.py's real-content input: the whole 4K HDR frame in the planar
+    10-bit layout, equal to the subsampled fixture's pixels where they meet."""
+    import os
+    import numpy as np
+    from hdr2sdr.synth import frames_from_rgb8
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    full = np.load(os.path.join(golden, 'website_hdr_full.npz'))['hdr']
+    sub = np.load(os.path.join(golden, 'website_frames.npz'))['hdr']
+    assert full.shape == (2160, 3840, 3) and np.array_equal(full[4::8, 4::8], sub)
+    fb = frames_from_rgb8(full, 2, 10, 'cpu')
+    assert (fb.width, fb.height, fb.nframes) == (3840, 2160, 2)
+    y = fb.y.numpy()
+    assert y.min() >= 64 and y.max() <= 940 and np.array_equal(y[0], y[1])
