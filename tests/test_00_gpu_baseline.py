@@ -1,0 +1,57 @@
+"""BASELINE.json's five configurations on the HIP path, first in the `-m gpu`
+run (this file sorts before every other test module), so that a `-x` stop
+later in the suite cannot hide them:
+
+* full-size frames of C1-C5 (1080p Reinhard + 33^3 at 8 bits; 4K Hable +
+  65^3 + eq 2.2; 4K BT.2390 on the libplacebo branch; 4K Mobius; 8K 12-bit
+  HLG Hable 12-bit out) against the CPU oracle, integer tolerance as
+  tests/test_gpu_parity.py's assert_close_int;
+* the tile kernel's own float stages (k_tile debug instances, the arithmetic
+  h2s_process runs) for the same configurations at 1e-3 relative, per stage.
+
+Reference anchors: the CPU chain src/utils.py:38-42 (C1, C2, C4, C5), the
+libplacebo chain src/utils.py:392-471 (C3), the output formats
+src/ffmpeg_command.py:355-360."""
+import pytest
+
+import hdr2sdr
+
+from test_gpu_parity import assert_close_int, check_float_stage, run_both
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def tm():
+    t = hdr2sdr.Tonemapper(0)
+    yield t
+    t.close()
+
+
+@pytest.mark.parametrize('name,kw,W,H,nframes', [
+    ('C1_1080p_reinhard_33_8bit', dict(tonemapper='reinhard', gamma=1.0, bits_out=8), 1920, 1080, 1),
+    ('C2_4k_hable_g22', dict(tonemapper='hable', gamma=2.2, bits_out=10), 3840, 2160, 2),
+    ('C3_4k_bt2390', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('4k_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('C4_4k_mobius', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 1),
+    ('C5_8k_hlg12_hable', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
+     7680, 4320, 1),
+])
+def test_full_size_configs(tm, name, kw, W, H, nframes):
+    params = hdr2sdr.TonemapParams(**kw)
+    got, want, _ = run_both(tm, params, 'smooth', W, H, nframes=nframes, lut_n=33 if name.startswith('C1') else 65)
+    assert_close_int(params, got, want, W, H)
+
+
+def test_full_size_uniform_worst_case(tm):
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=10)
+    got, want, _ = run_both(tm, params, 'uniform', 3840, 2160, nframes=1)
+    assert_close_int(params, got, want, 3840, 2160)
+
+
+# the BASELINE configurations among test_gpu_parity.FLOAT_CFGS, on the tile kernel
+@pytest.mark.parametrize('stage', [1, 2, 3, 4, 5])
+@pytest.mark.parametrize('kind', ['ramp', 'uniform'])
+@pytest.mark.parametrize('cfg', ['C2_hable_pq10', 'C3_bt2390_libplacebo', 'C4_mobius_native', 'C5_hable_hlg12'])
+def test_tile_kernel_float_stages(tm, cfg, kind, stage):
+    check_float_stage(tm, 'k_tile', cfg, kind, stage)

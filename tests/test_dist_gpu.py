@@ -23,23 +23,35 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _params(dynamic):
+# case -> (params, frames, W, H, bits_in): the C2-shaped static case, the one
+# exchange step (libplacebo peak_detect=1), and BASELINE's two 8-GPU configs at
+# full frame size: C4 (4K Mobius, frame-sharded) and C5 (8K 12-bit HLG, Hable
+# + 65^3, 12-bit out)
+CASES = {
+    'hable': (dict(tonemapper='hable', gamma=2.2), NF, W, H, 10),
+    'bt2390-peak-detect': (dict(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0), 6, W, H, 10),
+    'C4-4k-mobius': (dict(tonemapper='mobius', gamma=1.0, bits_out=10), 4, 3840, 2160, 10),
+    'C5-8k-hlg12-hable': (dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
+                          2, 7680, 4320, 12),
+}
+
+
+def _params(case):
     import hdr2sdr
-    if dynamic:   # libplacebo branch with peak_detect=1: the one exchange step
-        return hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0)
-    return hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2)
+    return hdr2sdr.TonemapParams(**CASES[case][0])
 
 
-def _frames(dynamic, a, b):
+def _frames(case, a, b):
     """global frames [a, b) of the test sequence, on the host"""
     from hdr2sdr.synth import synth_frames
     from test_peak_detect import sequence
-    if dynamic:
-        return np.ascontiguousarray(sequence(W, H)[a:b])
-    return synth_frames('smooth', b - a, W, H, 10, device='cpu', seed=0x5EED + a).to_numpy().buf
+    _, _, w, h, bits = CASES[case]
+    if case == 'bt2390-peak-detect':
+        return np.ascontiguousarray(sequence(w, h)[a:b])
+    return synth_frames('smooth', b - a, w, h, bits, device='cpu', seed=0x5EED + a).to_numpy().buf
 
 
-def _worker(rank, world, port, out_dir, dynamic):
+def _worker(rank, world, port, out_dir, case):
     for p in (os.path.join(REPO, 'hdr-to-sdr_amd'), REPO, HERE):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -52,18 +64,18 @@ def _worker(rank, world, port, out_dir, dynamic):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        params = _params(dynamic) if rank == 0 else None
+        params = _params(case) if rank == 0 else None
         lattice = hdr2sdr.generate_lattice(65) if rank == 0 else None
         params, lattice = broadcast_setup(params, lattice, 65)
-        n = 6 if dynamic else NF
+        _, n, w, h, bits = CASES[case]
         a, b = shard_range(n, world, rank)
         tm = hdr2sdr.Tonemapper(0, params, lattice)
-        shard = hdr2sdr.FrameBatch(_frames(dynamic, a, b), W, H, 10).to_torch('cuda:0')
-        if dynamic:
+        shard = hdr2sdr.FrameBatch(_frames(case, a, b), w, h, bits).to_torch('cuda:0')
+        if params.peak_detect:
             sync_peak_state(tm, shard, n)
         out = tm(shard)
         torch.cuda.synchronize()
-        px, total, _ = reduce_run((b - a) * W * H, frame_checksum(out.buf, a), 0.0)
+        px, total, _ = reduce_run((b - a) * w * h, frame_checksum(out.buf, a), 0.0)
         np.save(os.path.join(out_dir, f'r{rank}.npy'), np.array([px, total], dtype=np.int64))
         tm.close()
     finally:
@@ -71,22 +83,22 @@ def _worker(rank, world, port, out_dir, dynamic):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('dynamic', [False, True], ids=['hable', 'bt2390-peak-detect'])
-def test_two_ranks_on_libh2s_equal_one_process(tmp_path, dynamic):
+@pytest.mark.parametrize('case', sorted(CASES))
+def test_two_ranks_on_libh2s_equal_one_process(tmp_path, case):
     import torch
 
     import hdr2sdr
     from hdr2sdr.dist import frame_checksum
-    n = 6 if dynamic else NF
+    _, n, w, h, bits = CASES[case]
     world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), dynamic), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), case), nprocs=world, join=True,
                        start_method='spawn')
     res = [np.load(tmp_path / f'r{r}.npy') for r in range(world)]
-    tm = hdr2sdr.Tonemapper(0, _params(dynamic), hdr2sdr.generate_lattice(65))
-    want = tm(hdr2sdr.FrameBatch(_frames(dynamic, 0, n), W, H, 10).to_torch('cuda:0'))
+    tm = hdr2sdr.Tonemapper(0, _params(case), hdr2sdr.generate_lattice(65))
+    want = tm(hdr2sdr.FrameBatch(_frames(case, 0, n), w, h, bits).to_torch('cuda:0'))
     torch.cuda.synchronize()
     cks = frame_checksum(want.buf, 0)
     tm.close()
     for r in res:
-        assert int(r[0]) == n * W * H       # SUM of pixels over ranks
+        assert int(r[0]) == n * w * h       # SUM of pixels over ranks
         assert int(r[1]) == cks             # SUM of shard checksums == the one-process checksum

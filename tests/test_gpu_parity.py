@@ -227,14 +227,20 @@ FLOAT_CFGS = {
 }
 
 
-@pytest.mark.parametrize('stage', [1, 2, 3, 4, 5])
-@pytest.mark.parametrize('kind', ['uniform', 'edges', 'ramp'])
-@pytest.mark.parametrize('cfg', sorted(FLOAT_CFGS))
-@pytest.mark.parametrize('kernel', ['k_tile', 'k_debug'])
-def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
+# Pixels excluded as ill-conditioned (see check_float_stage) and values that
+# pass only because of the absolute floor, per (kernel, config, content,
+# stage), are written to $H2S_FLOAT_REPORT (one JSON line each) when set, and
+# bounded here: the floor may carry at most FLOOR_ONLY_MAX of the values that
+# would otherwise fail 1e-3 relative.
+FLOOR_ONLY_MAX = 0.02
+
+
+def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
+    """One (kernel, config, content, stage) float check; returns its report."""
+    import json
+    import os
     from hdr2sdr import _abi
     params = hdr2sdr.TonemapParams(**FLOAT_CFGS[cfg])
-    W, H = 128, 64
     src = synth_frames(kind, 1, W, H, params.bits_in, device='cpu', seed=3)
     tm.set_params(params)
     tm.set_lut(lattice(65))
@@ -251,7 +257,13 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
     if stage == 3 and kernel == 'k_tile':
         want = np.clip(want, 0.0, 1.0)      # k_tile clamps x to [0, 1) before the power (lattice coordinate)
     q = oracle.quant_bits(op)
-    floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
+    # The 6e-4 floor on stages 3/4 belongs to k_tile's PQ EOTF table (its first
+    # segment); the generic kernel evaluates the EOTF with powf and keeps the
+    # round-1 floor of 1e-5 on every stage.
+    if kernel == 'k_tile':
+        floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
+    else:
+        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-5, 5: 1e-5}[stage]
     got = got.astype(np.float64)
     with np.errstate(invalid='ignore'):
         err = np.abs(got - want)
@@ -299,13 +311,13 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
             warnings.simplefilter('ignore', RuntimeWarning)     # all-NaN pixels ('edges' codes)
             gain = np.nanmax(np.abs(want), axis=0) / np.nanmax(np.abs(lin), axis=0)
         floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens
-    tol = (1e-3 + 4e-5 * kappa[None]) * np.abs(want) + floor
+    rel = (1e-3 + 4e-5 * kappa[None]) * np.abs(want)
+    tol = rel + floor
     if params.resolved_pipeline() == 'libplacebo' and params.lp_tone == 'ipt' and stage in (2, 3):
         # the IPT form's LMS -> RGB rows (absolute sums up to 5.3) turn the
         # LMS values' relative error into an absolute error on channels they
         # cancel to near zero (saturated colours).  The oracle and the generic
         # kernel evaluate that form in double, the tile kernel through its PQ
-        # encode / EOTF tables: LMS relative error <= EPS_IPT
         # encode / EOTF tables: LMS relative error <= EPS_IPT.  Next to black
         # the stage-1 floor matters more than it does for the max(R,G,B) gain:
         # the PQ re-encode of a nearly black LMS row is steep (ipt_floor)
@@ -316,6 +328,19 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
             m709 = np.array(oracle.BT2020_TO_BT709)
             w2, d2 = np.einsum('ck,khw->chw', m709, np.nan_to_num(w2)), np.einsum('ck,khw->chw', np.abs(m709), d2)
         tol = tol + (d2 if stage == 2 else lp_encode_spread(params, w2, d2))
+    # what the assertion actually rests on, over the kept values
+    with np.errstate(invalid='ignore', divide='ignore'):
+        beyond_rel = keep & (err > rel)                        # would fail 1e-3 (+ kappa term) alone
+        floor_only = beyond_rel & (err <= tol)                 # ... and pass through a floor / conditioning term
+        relerr = np.where(keep & ~beyond_rel & (np.abs(want) > 0), err / np.abs(want), 0.0)
+    report = dict(kernel=kernel, cfg=cfg, kind=kind, stage=stage, values=int(want.size),
+                  excluded_px=int(skip.sum()), excluded_frac=float(skip.mean()),
+                  floor_set_frac=float((keep & (np.broadcast_to(floor, want.shape) > rel)).sum() / max(1, keep.sum())),
+                  floor_only_frac=float(floor_only.sum() / max(1, keep.sum())),
+                  max_rel_err_rest=float(relerr.max(initial=0.0)))
+    if os.environ.get('H2S_FLOAT_REPORT'):
+        with open(os.environ['H2S_FLOAT_REPORT'], 'a') as fh:
+            fh.write(json.dumps(report) + '\n')
     if params.resolved_pipeline() == 'libplacebo' and stage >= 4:
         # after the 8-bit rgba download the values are quantised: 1e-3 holds
         # wherever both sides rounded the download alike; a float-rounding flip
@@ -327,12 +352,23 @@ def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
         flip = ((err > tol) & keep).any(axis=0)
         assert flip.mean() < 0.01, f'{flip.mean():.3%} of pixels off after the rgba8 download'
         assert (err[keep] <= lim).all(), f'max {float(err[keep].max()):.4g} > {lim:.4g}'
-        return
+        return report
     bad = (err > tol) & keep
     i = int(np.argmax(np.where(bad, err / tol, 0)))
     assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {float(np.max(floor)):g} '
                            f'({int(skip.sum())} ill-conditioned pixels excluded); worst: want '
                            f'{float(want.flat[i]):.6g} got {float(got.flat[i]):.6g}')
+    assert report['floor_only_frac'] <= FLOOR_ONLY_MAX, (
+        f'{report["floor_only_frac"]:.2%} of values pass only through the floor (bound {FLOOR_ONLY_MAX:.0%})')
+    return report
+
+
+@pytest.mark.parametrize('stage', [1, 2, 3, 4, 5])
+@pytest.mark.parametrize('kind', ['uniform', 'edges', 'ramp'])
+@pytest.mark.parametrize('cfg', sorted(FLOAT_CFGS))
+@pytest.mark.parametrize('kernel', ['k_tile', 'k_debug'])
+def test_float_intermediates_within_1e3(tm, kernel, cfg, kind, stage):
+    check_float_stage(tm, kernel, cfg, kind, stage)
 
 
 def test_host_memory_path_equals_device_path(tm):
@@ -451,28 +487,6 @@ def test_empty_and_negative_batches(tm):
     torch.cuda.synchronize()
     assert not bool((dst.buf[0] == 0x1234).all())
     assert bool((dst.buf[1] == 0x1234).all())
-
-
-# ---- BASELINE.json full sizes (the oracle is OpenMP C: whole frames in ~1 s)
-@pytest.mark.parametrize('name,kw,W,H,nframes', [
-    ('C2_4k_hable_g22', dict(tonemapper='hable', gamma=2.2, bits_out=10), 3840, 2160, 2),
-    ('C3_4k_bt2390', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 1),
-    ('4k_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 1),
-    ('C4_4k_mobius', dict(tonemapper='mobius', gamma=1.0, bits_out=10), 3840, 2160, 1),
-    ('C5_8k_hlg12_hable', dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'),
-     7680, 4320, 1),
-    ('C1_1080p_reinhard_8bit', dict(tonemapper='reinhard', gamma=1.0, bits_out=8), 1920, 1080, 1),
-])
-def test_full_size_configs(tm, name, kw, W, H, nframes):
-    params = hdr2sdr.TonemapParams(**kw)
-    got, want, _ = run_both(tm, params, 'smooth', W, H, nframes=nframes, lut_n=33 if name.startswith('C1') else 65)
-    assert_close_int(params, got, want, W, H)
-
-
-def test_full_size_uniform_worst_case(tm):
-    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=10)
-    got, want, _ = run_both(tm, params, 'uniform', 3840, 2160, nframes=1)
-    assert_close_int(params, got, want, 3840, 2160)
 
 
 def _padded_descriptor(buf, W, H, bits, ls_pad, fp_pad):
