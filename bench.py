@@ -57,6 +57,21 @@ def parse_args():
     return ap.parse_args()
 
 
+# BASELINE.json's multi-GPU configurations, measured sharded at every N
+# beside the C2 headline (frames per rank fixed: weak scaling):
+# C4 = configs[3] (512 x 4K Mobius at 8 GPUs: 64 frames per rank),
+# C5 = configs[4] (8K 12-bit HLG in, Hable + 65^3, 12-bit out).
+SHARDED = (
+    ('C4', 'C4: 3840x2160 PQ HDR10 yuv420p10le -> yuv420p10le, mobius + 65^3 tetrahedral LUT, mode compat8, '
+           '64 frames per rank (512 at 8 GPUs)',
+     dict(tonemapper='mobius', gamma=1.0, bits_in=10, bits_out=10), 3840, 2160, 64, 65),
+    ('C5', 'C5: 7680x4320 HLG yuv420p12le -> yuv420p12le, hable + 65^3 tetrahedral LUT, mode compat8, '
+           '16 frames per rank',
+     dict(tonemapper='hable', gamma=1.0, bits_in=12, bits_out=12, transfer='arib-std-b67'), 7680, 4320, 16, 65),
+)
+SHARDED_STEPS = 100
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -103,14 +118,33 @@ def cpu_baseline(params, lattice, width, height, budget_s):
             if el >= budget or n >= 1024:
                 return n, el
 
-    n, el = rate(cores, budget_s * 2 / 3)
-    n1, el1 = rate(1, budget_s / 3)
+    n, el = rate(cores, budget_s * 0.45)
+    n1, el1 = rate(1, budget_s * 0.2)
     mpx = n * width * height / el / 1e6
-    return {'value': round(mpx, 3), 'unit': 'Mpixel/s', 'cores': cores, 'kind': 'port',
-            'value_1thread': round(n1 * width * height / el1 / 1e6, 3),
-            'sample': f'{n} x {width}x{height} smooth frame(s) in {el:.1f} s on {cores} OpenMP threads, '
-                      f'{n1} in {el1:.1f} s on 1 thread (value_1thread); same chain/params; '
-                      f'oracle/h2s_oracle.c (C restatement of the ffmpeg chain, not ffmpeg)'}
+    rec = {'value': round(mpx, 3), 'unit': 'Mpixel/s', 'cores': cores, 'kind': 'port',
+           'value_1thread': round(n1 * width * height / el1 / 1e6, 3),
+           'sample': f'{n} x {width}x{height} smooth frame(s) in {el:.1f} s on {cores} OpenMP threads, '
+                     f'{n1} in {el1:.1f} s on 1 thread (value_1thread); same chain/params; '
+                     f'oracle/h2s_oracle.c (C restatement of the ffmpeg chain, not ffmpeg)'}
+    # BASELINE configs[0] (C1), the reference's own CPU case: 1920x1080 PQ,
+    # Reinhard + 33^3 LUT, eq gamma 1.0, 10-bit in -> 8-bit out (the
+    # reference's default bit_depth 8, src/conversion.py:42), chain
+    # src/utils.py:38-42
+    import hdr2sdr
+    c1p = hdr2sdr.TonemapParams(tonemapper='reinhard', gamma=1.0, bits_in=10, bits_out=8)
+    p, lattice = oracle.params_from(c1p.to_c()), hdr2sdr.generate_lattice(33)
+    width, height = 1920, 1080
+    src = synth_frames('smooth', 1, width, height, 10, device='cpu', seed=0x5EED).to_numpy()
+    buf = np.ascontiguousarray(src.buf)
+    n, el = rate(cores, budget_s * 0.25)
+    n1, el1 = rate(1, budget_s * 0.1)
+    rec['c1'] = {'value': round(n * width * height / el / 1e6, 3), 'unit': 'Mpixel/s', 'cores': cores,
+                 'kind': 'port', 'value_1thread': round(n1 * width * height / el1 / 1e6, 3),
+                 'frames_per_s': round(n / el, 2), 'frames_per_s_1thread': round(n1 / el1, 2),
+                 'workload': 'C1: 1920x1080 PQ yuv420p10le -> yuv420p, reinhard + 33^3 tetrahedral LUT, eq gamma 1.0',
+                 'sample': f'{n} x 1920x1080 smooth frame(s) in {el:.1f} s on {cores} OpenMP threads, '
+                           f'{n1} in {el1:.1f} s on 1 thread'}
+    return rec
 
 
 def pmc_traffic(workload):
@@ -151,10 +185,20 @@ def dry_run(args, world, rank):
     px, cks, el = (b - a) * args.width * args.height, 0, 0.001 * (rank + 1)
     if world > 1:
         px, cks, el = reduce_run(px, cks, el)
+    # the sharded C4 / C5 lines: same shard and reduction flow, no GPU work
+    sharded = {}
+    for tag, workload, kw, w_, h_, fpr, _ in SHARDED:
+        a_, b_ = shard_range(world * fpr, world, rank)
+        px_, _, el_ = (b_ - a_) * w_ * h_, 0, 0.001 * (rank + 1)
+        if world > 1:
+            px_, _, el_ = reduce_run(px_, 0, el_)
+        sharded[tag] = {'workload': workload, 'pixels': px_, 'max_elapsed_s': el_, 'frames_total': world * fpr}
+    if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({'dry_run': True, 'n_gpus': args.gpus, 'world_size': seen, 'pixels': px,
-                          'max_elapsed_s': el, 'gamma': params.gamma, 'lattice_sum': float(lat.sum())}), flush=True)
+                          'max_elapsed_s': el, 'gamma': params.gamma, 'lattice_sum': float(lat.sum()),
+                          'config': {'workload': 'C2 (dry run)', 'sharded_configs': sharded}}), flush=True)
 
 
 def main():
@@ -326,6 +370,50 @@ def main():
             t_.close()
             del src_, dst_
 
+    # BASELINE's multi-GPU configurations C4 / C5, frame-sharded over every
+    # rank exactly as the headline (barrier + synchronize around the timed
+    # launches, MAX of the elapsed time over ranks, SUM of pixels)
+    sharded = {}
+    for tag, workload, kw, w_, h_, fpr, lut_n in SHARDED:
+        p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
+        lat_ = hdr2sdr.generate_lattice(lut_n) if rank == 0 else None
+        if world > 1:
+            p_, lat_ = broadcast_setup(p_ if rank == 0 else None, lat_, lut_n, dev)
+        t_ = hdr2sdr.Tonemapper(local, p_, lat_)
+        a_, b_ = shard_range(world * fpr, world, rank)
+        src_ = synth_frames('smooth', b_ - a_, w_, h_, p_.bits_in, device=dev, seed=0x5EED + a_)
+        dst_ = hdr2sdr.FrameBatch.empty_torch(b_ - a_, w_, h_, p_.bits_out, dev)
+        st_ = torch.cuda.current_stream(dev)
+        for _ in range(3):
+            t_.process(src_, dst_, st_)
+        torch.cuda.synchronize(dev)
+        t_.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0_ = time.perf_counter()
+        for _ in range(SHARDED_STEPS):
+            t_.process(src_, dst_, st_)
+        torch.cuda.synchronize(dev)
+        el_ = time.perf_counter() - t0_
+        if world > 1:
+            dist.barrier()
+        kms_ = t_.kernel_ms(SHARDED_STEPS)
+        t_.set_timing(False)
+        px_ = (b_ - a_) * w_ * h_ * SHARDED_STEPS
+        cks_ = frame_checksum(dst_.buf, a_)
+        if world > 1:
+            px_, cks_, el_ = reduce_run(px_, cks_, el_, dev)
+        b_px = 1.5 * (1 if p_.bits_in == 8 else 2) + 1.5 * (1 if p_.bits_out == 8 else 2)
+        sharded[tag] = {'workload': workload, 'value': round(px_ / el_ / 1e6, 1), 'unit': 'Mpixel/s',
+                        'ms_per_step': round(el_ / SHARDED_STEPS * 1e3, 4), 'steps': SHARDED_STEPS,
+                        'frames_total': world * fpr, 'frames_per_rank': fpr,
+                        'rank0_kernel_ms': round(kms_, 4),
+                        'rank0_hbm_frac': round(b_px * (b_ - a_) * w_ * h_ / (kms_ / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                        'output_checksum': cks_}
+        t_.close()
+        del src_, dst_
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -363,6 +451,7 @@ def main():
             'alt_content': alt,
             'real_content': real,
             'other_configs': other,
+            'sharded_configs': sharded,
             'host_path': host_path,
         },
         'roofline': {

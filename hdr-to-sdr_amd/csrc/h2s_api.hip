@@ -51,6 +51,7 @@ struct h2s_ctx {
   bool fast_enabled = true;
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
+  int kernel = 0;           // 0: k_tile, 1: k_wave (H2S_KERNEL=tile|wave)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
@@ -75,7 +76,12 @@ struct h2s_ctx {
   // their own streams (two DMA directions overlap the kernel and each other)
   hipStream_t ps[3] = {};
   hipEvent_t pev[2 * kMaxChunks + 2] = {};
-  bool launched = false;         // work queued since the last set_params / set_lut drain
+  // events recorded after this context's own asynchronous launches, on the
+  // streams they went to: set_params / set_lut wait for exactly these (no
+  // device-wide synchronisation), then recycle them
+  std::vector<hipEvent_t> pend, ev_free;
+  hipEvent_t chr_ev = nullptr;   // after the last BICUBIC two-pass launch (d_chr scratch in use)
+  bool chr_pending = false;
   float2* d_chr = nullptr;       // BICUBIC chroma: one frame's per-pixel (Cb, Cr)
   size_t chr_cap = 0;
 };
@@ -159,6 +165,24 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
     return fail(c, H2S_E_INVALID_ARG, "target_black must be >= 0");
   if (!isnan(p->target_black) && !isnan(p->target_white) && !(p->target_black < p->target_white))
     return fail(c, H2S_E_INVALID_ARG, "target_black must be below target_white");
+  if (p->lp_range != H2S_LP_RANGE_FULL && p->lp_range != H2S_LP_RANGE_LIMITED)
+    return fail(c, H2S_E_INVALID_ARG, "unknown lp_range");
+  if (p->lp_dither != H2S_LP_DITHER_NONE && p->lp_dither != H2S_LP_DITHER_ORDERED)
+    return fail(c, H2S_E_INVALID_ARG, "unknown lp_dither");
+  if (p->lp_p010 != H2S_LP_P010_KEEP && p->lp_p010 != H2S_LP_P010_TRUNCATE)
+    return fail(c, H2S_E_INVALID_ARG, "unknown lp_p010");
+  // vf_libplacebo's option ranges (smoothing_period 0..1000, scene thresholds
+  // -1..100 (negative: scene detection off), percentile 0..100, minimum_peak 0..100)
+  if (!isnan(p->pd_smoothing) && !(p->pd_smoothing >= 0.0 && p->pd_smoothing <= 1000.0))
+    return fail(c, H2S_E_INVALID_ARG, "pd_smoothing must be in [0, 1000] frames");
+  if (!isnan(p->pd_scene_low) && !(p->pd_scene_low >= -1.0 && p->pd_scene_low <= 100.0))
+    return fail(c, H2S_E_INVALID_ARG, "pd_scene_low must be in [-1, 100]");
+  if (!isnan(p->pd_scene_high) && !(p->pd_scene_high >= -1.0 && p->pd_scene_high <= 100.0))
+    return fail(c, H2S_E_INVALID_ARG, "pd_scene_high must be in [-1, 100]");
+  if (!isnan(p->pd_percentile) && !(p->pd_percentile > 0.0 && p->pd_percentile <= 100.0))
+    return fail(c, H2S_E_INVALID_ARG, "pd_percentile must be in (0, 100]");
+  if (!isnan(p->pd_min_peak) && !(p->pd_min_peak >= 0.0 && p->pd_min_peak <= 100.0))
+    return fail(c, H2S_E_INVALID_ARG, "pd_min_peak must be in [0, 100]");
   return 0;
 }
 
@@ -528,8 +552,8 @@ bool vec_ok(const h2s_frames* f, bool out8) {
 
 // tile kernel: at least one 64-pixel tile, every row start 16-B aligned (8-B
 // for 8-bit chroma output)
-bool tile_ok(const h2s_frames* in, const h2s_frames* out, bool out8) {
-  if (in->width < 64) return false;  // width % 64 columns go to k_process (launch_chain)
+bool tile_ok(const h2s_frames* in, const h2s_frames* out, bool out8, int tw) {
+  if (in->width < tw) return false;  // width % tw columns go to k_process (launch_chain)
   for (int p = 0; p < 3; p++) {
     if (!aligned(in->data[p], 16) || in->linesize[p] % 16 || in->frame_pitch[p] % 16) return false;
     const long long a = out8 ? (p ? 8 : 8) : 16;
@@ -641,6 +665,10 @@ void h2s_params_default(h2s_params* p) {
   p->chroma_edge = H2S_EDGE_ZIMG;
   p->lut_input = H2S_LUT_IN_FLOAT;
   p->lp_tone = H2S_LP_TONE_IPT;   // libplacebo >= 6 tone-maps in IPT (h2s.h enum h2s_lp_tone)
+  p->lp_range = H2S_LP_RANGE_FULL;
+  p->lp_dither = H2S_LP_DITHER_NONE;
+  p->lp_p010 = H2S_LP_P010_KEEP;
+  p->pd_smoothing = p->pd_scene_low = p->pd_scene_high = p->pd_percentile = p->pd_min_peak = NAN;
 }
 
 int h2s_create(int device, h2s_ctx** out) {
@@ -655,6 +683,7 @@ int h2s_create(int device, h2s_ctx** out) {
   c->device = device;
   h2s_params_default(&c->params);
   if (const char* v = getenv("H2S_HOST_SERIAL")) c->serial_host = atoi(v) != 0;
+  if (const char* v = getenv("H2S_KERNEL")) c->kernel = strcmp(v, "wave") == 0 ? 1 : 0;
   if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
     const int tpb = atoi(v);
     if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
@@ -678,6 +707,9 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_curve) hipFree(c->d_curve);
   if (c->d_chr) hipFree(c->d_chr);
   if (c->curve_ev) hipEventDestroy(c->curve_ev);
+  if (c->chr_ev) hipEventDestroy(c->chr_ev);
+  for (hipEvent_t ev : c->pend) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_free) hipEventDestroy(ev);
   for (int i = 0; i < kEvRing; i++) {
     if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
     if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
@@ -689,13 +721,45 @@ void h2s_destroy(h2s_ctx* c) {
   delete c;
 }
 
-// set_params / set_lut rewrite device tables that kernels already queued on
-// any stream may still read: drain the device first (include/h2s.h)
+// set_params / set_lut rewrite device tables that this context's queued
+// kernels may still read: wait for the events recorded after its own
+// launches (include/h2s.h), not for the device
 static int drain_launches(h2s_ctx* c) {
-  if (!c->launched) return 0;
-  hipError_t e = hipDeviceSynchronize();
+  hipError_t e = hipSuccess;
+  for (hipEvent_t ev : c->pend) {
+    const hipError_t r = hipEventSynchronize(ev);
+    if (e == hipSuccess) e = r;
+    c->ev_free.push_back(ev);
+  }
+  c->pend.clear();
   if (e != hipSuccess) return hip_fail(c, e, "draining queued launches");
-  c->launched = false;
+  return 0;
+}
+
+// record that this context queued work on stream s (after the launches)
+static int note_launch(h2s_ctx* c, hipStream_t s) {
+  if (c->pend.size() >= 32) {   // recycle the events that have completed
+    size_t j = 0;
+    for (size_t i = 0; i < c->pend.size(); i++) {
+      if (hipEventQuery(c->pend[i]) == hipSuccess) c->ev_free.push_back(c->pend[i]);
+      else c->pend[j++] = c->pend[i];
+    }
+    c->pend.resize(j);
+  }
+  hipEvent_t ev = nullptr;
+  if (!c->ev_free.empty()) {
+    ev = c->ev_free.back();
+    c->ev_free.pop_back();
+  } else {
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "launch event");
+  }
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) {
+    c->ev_free.push_back(ev);
+    return hip_fail(c, e, "launch event");
+  }
+  c->pend.push_back(ev);
   return 0;
 }
 
@@ -921,8 +985,8 @@ static int prepare(h2s_ctx* c, KParams* k, bool need_lut = true) {
 
 // the generic kernel over the columns right of the last whole 64-pixel tile
 // (left-sited chroma needs no left neighbour, so the seam is exact)
-static hipError_t launch_tail(const KParams& k, int nframes, bool vec, bool out8, hipStream_t s) {
-  const int w64 = k.W & ~63;
+static hipError_t launch_tail(const KParams& k, int nframes, bool vec, bool out8, hipStream_t s, int tw) {
+  const int w64 = k.W & ~(tw - 1);
   KParams kt = k;
   kt.gx0 = w64 / 8;
   kt.ngx = (k.cw - w64 / 2 + 3) / 4;
@@ -986,7 +1050,8 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   }
   // k_tile covers the whole 64-pixel tiles; the chroma right halo of its last
   // tile reads the real column (F.cw stays the frame's), so the split is exact
-  const int w64 = k.W & ~63;
+  const int tw = c->kernel ? h2s::WTW : h2s::TBW;
+  const int w64 = k.W & ~(tw - 1);
   F.W = w64, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
   F.chroma_edge = k.chroma_edge;
   for (int p = 0; p < 3; p++) {
@@ -994,8 +1059,9 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
     F.in_bytes[p] = (int)(ib < 0x7fffffff ? ib : 0x7fffffff);
     F.out_bytes[p] = (int)(ob < 0x7fffffff ? ob : 0x7fffffff);
   }
-  F.nbx = (unsigned)(w64 / 64);
-  F.nby = (unsigned)((k.H + 31) / 32);
+  F.kernel = c->kernel;
+  F.nbx = (unsigned)(w64 / tw);
+  F.nby = (unsigned)(c->kernel ? (k.H + h2s::WTH - 1) / h2s::WTH : (k.H + h2s::TBH - 1) / h2s::TBH);
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
   F.cv_frames = cvf;
@@ -1006,7 +1072,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
   hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.pipe == h2s::PIPE_LIBPLACEBO ? 1 : 0, s, dbg);
   if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
-  return launch_tail(k, nframes, vec, out8, s);
+  return launch_tail(k, nframes, vec, out8, s, tw);
 }
 
 // the tile kernel serves: both of the reference's chains (the CPU chain, and
@@ -1028,8 +1094,9 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
 
 static int choose_path(const h2s_ctx* c, const KParams& k, const h2s_frames* din, const h2s_frames* dout,
                        bool out8) {
-  if (fast_params_ok(c, k) && tile_ok(din, dout, out8))
-    return (din->width & 63) ? H2S_PATH_TILE_TAIL : H2S_PATH_TILE;
+  const int tw = c->kernel ? h2s::WTW : h2s::TBW;
+  if (fast_params_ok(c, k) && tile_ok(din, dout, out8, tw))
+    return (din->width & (tw - 1)) ? H2S_PATH_TILE_TAIL : H2S_PATH_TILE;
   return c->params.chroma_filter == H2S_CHROMA_BICUBIC ? H2S_PATH_TWO_PASS : H2S_PATH_GENERIC;
 }
 
@@ -1155,10 +1222,10 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
     if (e == hipSuccess) e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
     if (e == hipSuccess) e = hipEventRecord(c->curve_ev, s);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
-    if ((k.W & 63) == 0) return 0;
+    if ((k.W & ((c->kernel ? h2s::WTW : h2s::TBW) - 1)) == 0) return 0;
   }
   for (int f = 0; f < nframes; f++) {
-    e = fast ? launch_tail(kfs[f], 1, vec, out8, s) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
+    e = fast ? launch_tail(kfs[f], 1, vec, out8, s, c->kernel ? h2s::WTW : h2s::TBW) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   }
   return 0;
@@ -1336,8 +1403,22 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   const int path = choose_path(c, k, &din, &dout, out8);
   const bool fast = path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL;
   if (fast && k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) return rc;
-  if (path == H2S_PATH_TWO_PASS && (rc = ensure_chr(c, k))) return rc;
-  c->launched = true;
+  if (path == H2S_PATH_TWO_PASS) {
+    if ((rc = ensure_chr(c, k))) return rc;
+    // one context scratch (d_chr) for every two-pass launch: a launch on
+    // another stream waits until the previous one has finished with it
+    if (!c->chr_ev) {
+      hipError_t e = hipEventCreateWithFlags(&c->chr_ev, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        c->chr_ev = nullptr;
+        return hip_fail(c, e, "two-pass event");
+      }
+    }
+    if (c->chr_pending) {
+      hipError_t e = hipStreamWaitEvent(s, c->chr_ev, 0);
+      if (e != hipSuccess) return hip_fail(c, e, "two-pass ordering");
+    }
+  }
   const bool dyn_peak = c->params.peak_detect &&
                         (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE || k.pipe == h2s::PIPE_LIBPLACEBO);
   // the dynamic peak walks frames in order with a host round trip per frame,
@@ -1372,11 +1453,16 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     e = copy_frames(out, &dout, nframes, s);
     if (e != hipSuccess) return hip_fail(c, e, "device->host copy");
   }
+  if (path == H2S_PATH_TWO_PASS) {
+    if ((e = hipEventRecord(c->chr_ev, s)) != hipSuccess) return hip_fail(c, e, "two-pass event");
+    c->chr_pending = true;
+  }
   if (host_in || host_out) {
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(c, e, "stream synchronize");
+    return 0;
   }
-  return 0;
+  return note_launch(c, s);
 }
 
 int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb, int out_location,
@@ -1425,7 +1511,6 @@ int h2s_debug_float(h2s_ctx* c, const h2s_frames* in, int stage, float* out_rgb,
     }
     e = launch_chain(c, k, true, false, out8, 1, s, nullptr, false, stage, dout);
   }
-  c->launched = true;
   if (e == hipSuccess && out_location == H2S_LOC_HOST) e = hipMemcpyAsync(out_rgb, dout, ob, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   hipStreamSynchronize(s);

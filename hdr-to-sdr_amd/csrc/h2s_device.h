@@ -113,6 +113,7 @@ struct FastParams : CurveConsts {
   int chroma_edge;                 // S1 upsampler edge rule (chroma_edge_at)
   unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
   int tpb;                         // tiles walked by one block (k_tile prefetches tile i+1 during tile i)
+  int kernel;                      // 0: k_tile (64 x 32 tiles per block), 1: k_wave (32 x 16 tiles per wave)
   const uint8_t* in[3];
   long long in_ls[3], in_fp[3];
   uint8_t* out[3];
@@ -171,6 +172,8 @@ struct FastParams : CurveConsts {
   float inv_nm1;
 };
 
+constexpr int TBW = 64, TBH = 32;   // k_tile: luma tile of one block
+constexpr int WTW = 32, WTH = 16;   // k_wave: luma tile of one wave
 constexpr int PQ_SEG = 128;          // segments per unit of E
 constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
 constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path

@@ -34,10 +34,13 @@ EXPAND_SHIFT, EXPAND_REPLICATE = 0, 1
 EDGE_ZIMG, EDGE_REPLICATE, EDGE_MIRROR = 0, 1, 2
 LUT_IN_FLOAT, LUT_IN_RGB48 = 0, 1
 LP_TONE_IPT, LP_TONE_MAX_RGB = 0, 1
+LP_RANGE_FULL, LP_RANGE_LIMITED = 0, 1
+LP_DITHER_NONE, LP_DITHER_ORDERED = 0, 1
+LP_P010_KEEP, LP_P010_TRUNCATE = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
 OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/h2s.h declares (checked by tests/test_abi_exports.py)
 EXPORTS = (
@@ -75,7 +78,13 @@ class H2SParams(ctypes.Structure):
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
         ('lut_input', ctypes.c_int32),
-        ('lp_tone', ctypes.c_int32), ('reserved', ctypes.c_int32 * 1),
+        ('lp_tone', ctypes.c_int32),
+        # ABI v3: libplacebo branch options and peak_detect parameters
+        ('lp_range', ctypes.c_int32), ('lp_dither', ctypes.c_int32), ('lp_p010', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 2),
+        ('pd_smoothing', ctypes.c_double), ('pd_scene_low', ctypes.c_double),
+        ('pd_scene_high', ctypes.c_double), ('pd_percentile', ctypes.c_double),
+        ('pd_min_peak', ctypes.c_double),
     ]
 
 

@@ -60,17 +60,31 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, 'h2s.h')]
     os.makedirs(OBJ_DIR, exist_ok=True)
     objs = [os.path.join(OBJ_DIR, os.path.basename(s) + '.o') for s in srcs]
-    todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + hdrs)]
+
+    def flags(s):
+        return [f'--offload-arch={ARCH}'] + CFLAGS + SOURCE_FLAGS.get(os.path.basename(s), [])
+
+    def cmd_stale(s, o):
+        # an object built with other flags (an ablation build, a changed
+        # CFLAGS / SOURCE_FLAGS entry) is stale whatever its mtime says
+        try:
+            with open(o + '.cmd') as fh:
+                return fh.read() != ' '.join(flags(s))
+        except OSError:
+            return True
+
+    todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + hdrs) or cmd_stale(s, o)]
 
     def compile_one(so):
         s, o = so
         tmp = o + f'.tmp{os.getpid()}'
-        cmd = [_hipcc(), f'--offload-arch={ARCH}'] + CFLAGS + SOURCE_FLAGS.get(os.path.basename(s), []) + \
-            ['-c', '-o', tmp, s]
+        cmd = [_hipcc()] + flags(s) + ['-c', '-o', tmp, s]
         if verbose:
             print(' '.join(cmd))
         subprocess.run(cmd, check=True)
         os.replace(tmp, o)
+        with open(o + '.cmd', 'w') as fh:
+            fh.write(' '.join(flags(s)))
 
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), int(os.environ.get('MAX_JOBS', '8'))))) as ex:
         list(ex.map(compile_one, todo))

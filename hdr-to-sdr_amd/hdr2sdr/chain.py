@@ -64,6 +64,10 @@ _LUT_IN = {'float': _abi.LUT_IN_FLOAT, 'rgb48': _abi.LUT_IN_RGB48}
 _LP_TONE = {'ipt': _abi.LP_TONE_IPT, 'max-rgb': _abi.LP_TONE_MAX_RGB}
 _EDGE = {'zimg': _abi.EDGE_ZIMG, 'replicate': _abi.EDGE_REPLICATE, 'mirror': _abi.EDGE_MIRROR}
 _PIPELINE = {'auto': _abi.PIPE_AUTO, 'cpu': _abi.PIPE_CPU_CHAIN, 'libplacebo': _abi.PIPE_LIBPLACEBO}
+# libplacebo stage options (include/h2s.h enum h2s_lp_range / _dither / _p010)
+_LP_RANGE = {'full': _abi.LP_RANGE_FULL, 'limited': _abi.LP_RANGE_LIMITED}
+_LP_DITHER = {'none': _abi.LP_DITHER_NONE, 'ordered': _abi.LP_DITHER_ORDERED}
+_LP_P010 = {'keep': _abi.LP_P010_KEEP, 'truncate': _abi.LP_P010_TRUNCATE}
 
 
 def is_gpu_only_tonemapper(tonemapper: str) -> bool:
@@ -103,6 +107,16 @@ class TonemapParams:
     chroma_edge: str = 'zimg'   # S1 upsampler edge rule ('zimg' | 'replicate' | 'mirror')
     lut_input: str = 'float'    # S3 -> S4 format on the CPU chain ('float' | 'rgb48')
     lp_tone: str = 'ipt'        # libplacebo branch: curve on IPT intensity | gain on max(R,G,B) ('ipt' | 'max-rgb')
+    # libplacebo branch options (include/h2s.h ABI v3; PARITY UNPINNED models)
+    lp_range: str = 'full'      # what range=tv does to the rgba download ('full' | 'limited')
+    lp_dither: str = 'none'     # the 8-bit download ('none' | 'ordered')
+    lp_p010: str = 'keep'       # 12-bit input through format=p010 ('keep' | 'truncate')
+    # peak_detect=1 parameters (NaN: vf_libplacebo's defaults 100 / 5.5 / 10 / 99.995 / 1.0)
+    pd_smoothing: float = math.nan
+    pd_scene_low: float = math.nan
+    pd_scene_high: float = math.nan
+    pd_percentile: float = math.nan
+    pd_min_peak: float = math.nan
 
     def __post_init__(self) -> None:
         tm = self.tonemapper.lower()
@@ -115,7 +129,8 @@ class TonemapParams:
         if self.desat_luma not in _DESAT_LUMA:
             raise ValueError(f'unknown desat_luma {self.desat_luma!r}')
         for name, table in (('chroma_filter', _CHROMA), ('dither', _DITHER), ('expand', _EXPAND),
-                            ('pipeline', _PIPELINE), ('chroma_edge', _EDGE), ('lut_input', _LUT_IN), ('lp_tone', _LP_TONE)):
+                            ('pipeline', _PIPELINE), ('chroma_edge', _EDGE), ('lut_input', _LUT_IN), ('lp_tone', _LP_TONE),
+                            ('lp_range', _LP_RANGE), ('lp_dither', _LP_DITHER), ('lp_p010', _LP_P010)):
             if getattr(self, name) not in table:
                 raise ValueError(f'unknown {name} {getattr(self, name)!r}; expected one of {sorted(table)}')
         if self.pipeline == 'libplacebo' and tm not in LIBPLACEBO_TONEMAPPERS:
@@ -181,6 +196,14 @@ class TonemapParams:
         p.chroma_edge = _EDGE[self.chroma_edge]
         p.lut_input = _LUT_IN[self.lut_input]
         p.lp_tone = _LP_TONE[self.lp_tone]
+        p.lp_range = _LP_RANGE[self.lp_range]
+        p.lp_dither = _LP_DITHER[self.lp_dither]
+        p.lp_p010 = _LP_P010[self.lp_p010]
+        p.pd_smoothing = self.pd_smoothing
+        p.pd_scene_low = self.pd_scene_low
+        p.pd_scene_high = self.pd_scene_high
+        p.pd_percentile = self.pd_percentile
+        p.pd_min_peak = self.pd_min_peak
         return p
 
     def resolved_pipeline(self) -> str:
@@ -225,6 +248,34 @@ def _split_filters(chain: str) -> 'list[tuple[str, dict[str, str], list[str]]]':
     return out
 
 
+# libplacebo stage options build_libplacebo_filter emits (src/utils.py:445-449)
+# and the values the engine models; anything else is rejected rather than
+# converted with a behaviour the string did not ask for
+_LP_OPTION_VALUES = {
+    'w': {'iw'}, 'h': {'ih'},                  # output size = input size (scaling is the preview's)
+    'colorspace': {'bt709'},
+    'color_primaries': {'auto', 'bt709'},      # with / without the lut3d stage (checked after the loop)
+    'color_trc': {'bt709'},
+    'range': {'tv', 'pc'},                     # tv: the lp_range model; pc: full range
+    'peak_detect': {'0', '1', 'true', 'false'},
+    'format': {'rgba', 'nv12'},                # with / without the lut3d stage
+}
+
+
+def _check_libplacebo_options(kv: 'dict[str, str]', pos: 'list[str]') -> None:
+    if pos:
+        raise ValueError(f'libplacebo positional options {pos} are not modelled')
+    for k, v in kv.items():
+        if k == 'tonemapping':
+            continue
+        allowed = _LP_OPTION_VALUES.get(k)
+        if allowed is None:
+            raise ValueError(f'libplacebo option {k}={v} is not modelled '
+                             f'(the reference sets {sorted(_LP_OPTION_VALUES)} and tonemapping)')
+        if v not in allowed:
+            raise ValueError(f'libplacebo {k}={v} is not modelled (accepted: {sorted(allowed)})')
+
+
 def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
                        transfer: str = 'smpte2084', **overrides: Any) -> 'tuple[TonemapParams, str | None]':
     """Parse a reference chain string into (params, lut_path).
@@ -241,6 +292,7 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
                                 lut_enabled=False)
     lut_path = None
     seen_linear = False
+    lp_primaries = lp_format = None
     for name, kv, pos in _split_filters(chain):
         if name == 'zscale':
             t = kv.get('t', kv.get('transfer'))
@@ -289,6 +341,7 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
                 # mobius (NORM scaling) are restated beside bt.2390 / spline
                 raise ValueError(f'libplacebo tonemapping={tm} is not supported '
                                  f'(the reference names {sorted(LIBPLACEBO_TONEMAPPERS)})')
+            _check_libplacebo_options(kv, pos)
             seen_linear = True
             kw['tonemapper'] = tm.lower()
             kw['desat'] = 0.0
@@ -296,6 +349,10 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             # peak_detect=1 (src/utils.py:448): per-frame detected, temporally
             # smoothed source peak (every libplacebo operator: it sets the source range)
             kw['peak_detect'] = kv.get('peak_detect', '0') in ('1', 'true')
+            if kv.get('range') == 'pc':
+                kw['lp_range'] = 'full'          # full-range output: no model choice left
+            lp_primaries = kv.get('color_primaries')
+            lp_format = kv.get('format')
         elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
             continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)
         elif name == 'eq':
@@ -306,5 +363,16 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
             raise ValueError(f'filter {name!r} is outside the tone-mapping hot path')
     if not seen_linear or 'tonemapper' not in kw:
         raise ValueError('not a tone-mapping chain (needs zscale=t=linear and tonemap=)')
+    if kw.get('pipeline') == 'libplacebo':
+        # the reference pairs color_primaries=auto + format=rgba with its lut3d
+        # stage and color_primaries=bt709 + format=nv12 without it
+        # (src/utils.py:432-444); the other pairings are not modelled
+        # (absent options take vf_libplacebo's defaults: primaries 'auto' =
+        # the input's; format = whatever the following format= filter picks)
+        want = ('auto', 'rgba') if kw['lut_enabled'] else ('bt709', 'nv12')
+        if (lp_primaries or 'auto') != want[0] or (lp_format or want[1]) != want[1]:
+            raise ValueError(f'libplacebo color_primaries={lp_primaries} format={lp_format} with the LUT '
+                             f'{"on" if kw["lut_enabled"] else "off"} is not modelled (the reference uses '
+                             f'color_primaries={want[0]}:format={want[1]})')
     kw.update(overrides)
     return TonemapParams(**kw), lut_path

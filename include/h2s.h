@@ -21,7 +21,9 @@
  * it is given when both frame sets live in device memory; the caller
  * synchronises.  h2s_set_params and h2s_set_lut first wait for every launch
  * the context has queued (on any stream) to finish, so replacing the tables a
- * kernel in flight reads is safe.
+ * kernel in flight reads is safe; they wait on events recorded after the
+ * context's own launches only, never on other contexts or on unrelated work
+ * on the device.
  *
  * Errors: 0 on success, a negative H2S_E_* code otherwise; the message is
  * available from h2s_last_error(ctx) (or h2s_last_error(NULL) for failures
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define H2S_ABI_VERSION 2
+#define H2S_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------- */
 #define H2S_OK 0
@@ -143,6 +145,27 @@ enum h2s_lut_input { H2S_LUT_IN_FLOAT = 0, H2S_LUT_IN_RGB48 = 1 };
  * MAX_RGB: gain curve(max RGB) / max RGB on R, G, B (the round-2 model). */
 enum h2s_lp_tone { H2S_LP_TONE_IPT = 0, H2S_LP_TONE_MAX_RGB = 1 };
 
+/* libplacebo branch: the open options of the reference's stage
+ * `libplacebo=...:range=tv:peak_detect=1:format=rgba` (src/utils.py:445-449),
+ * each a named model (SURVEY.md App. B style; PARITY UNPINNED, libplacebo and
+ * vf_libplacebo are absent from the image).
+ * h2s_lp_range: FULL = the rgba download carries full-range codes
+ *   round(255 v) (libplacebo ignores range= for an RGB output); LIMITED =
+ *   range=tv applies to the RGB output: round(16 + 219 v), which lut3d and
+ *   the auto-scale to -pix_fmt then read as full-range RGB.
+ * h2s_lp_dither: NONE = the 8-bit download rounds to nearest; ORDERED = a
+ *   16 x 16 Bayer matrix offsets each code before the truncation (a stand-in
+ *   for libplacebo's default dither, whose blue-noise texture is not
+ *   restated: it measures how much the dither matters).
+ * h2s_lp_p010: the reference uploads through `format=p010` (src/utils.py:
+ *   430-431).  KEEP = a 12-bit input reaches libplacebo at full precision
+ *   (swscale's planar -> P01x path shifts the 12-bit code into the high bits,
+ *   code << 4, and the low bits are read as fraction); TRUNCATE = the 10-bit
+ *   container drops the two low bits (code & ~3).  10-bit input: no effect. */
+enum h2s_lp_range { H2S_LP_RANGE_FULL = 0, H2S_LP_RANGE_LIMITED = 1 };
+enum h2s_lp_dither { H2S_LP_DITHER_NONE = 0, H2S_LP_DITHER_ORDERED = 1 };
+enum h2s_lp_p010 { H2S_LP_P010_KEEP = 0, H2S_LP_P010_TRUNCATE = 1 };
+
 /* S8 8-bit -> bits_out expansion after eq. */
 enum h2s_expand { H2S_EXPAND_SHIFT = 0, H2S_EXPAND_REPLICATE = 1 };
 
@@ -217,7 +240,20 @@ typedef struct h2s_params {
   int32_t chroma_edge;   /* enum h2s_chroma_edge (S1)                       */
   int32_t lut_input;     /* enum h2s_lut_input (S3 -> S4, CPU chain)        */
   int32_t lp_tone;       /* enum h2s_lp_tone (libplacebo branch)            */
-  int32_t reserved[1];
+  /* ABI v3: libplacebo branch options (enums above) */
+  int32_t lp_range;      /* enum h2s_lp_range                               */
+  int32_t lp_dither;     /* enum h2s_lp_dither                              */
+  int32_t lp_p010;       /* enum h2s_lp_p010                                */
+  int32_t reserved[2];   /* keeps the doubles below 8-byte aligned        */
+  /* peak_detect=1 (libplacebo's pl_peak_detect_params as vf_libplacebo sets
+   * them; NaN = vf_libplacebo's option defaults, in brackets):            */
+  double pd_smoothing;   /* IIR smoothing period, frames [100]              */
+  double pd_scene_low;   /* scene-change thresholds on the frame average,   */
+  double pd_scene_high;  /*   % of the PQ range [5.5, 10]                   */
+  double pd_percentile;  /* detected peak = this percentile of per-pixel
+                          * PQ(max R,G,B); 100 = the maximum [99.995]       */
+  double pd_min_peak;    /* lower bound on the detected peak, relative to
+                          * the SDR target white [1.0]                      */
 } h2s_params;
 
 /* A batch of planar 4:2:0 frames (yuv420p / yuv420p10le / yuv420p12le).

@@ -50,7 +50,13 @@ class Params(ctypes.Structure):
         ('target_white', ctypes.c_double),
         ('chroma_edge', ctypes.c_int32),
         ('lut_input', ctypes.c_int32),
-        ('lp_tone', ctypes.c_int32), ('reserved', ctypes.c_int32 * 1),
+        ('lp_tone', ctypes.c_int32),
+        # ABI v3: libplacebo branch options and peak_detect parameters
+        ('lp_range', ctypes.c_int32), ('lp_dither', ctypes.c_int32), ('lp_p010', ctypes.c_int32),
+        ('reserved', ctypes.c_int32 * 2),
+        ('pd_smoothing', ctypes.c_double), ('pd_scene_low', ctypes.c_double),
+        ('pd_scene_high', ctypes.c_double), ('pd_percentile', ctypes.c_double),
+        ('pd_min_peak', ctypes.c_double),
     ]
 
 

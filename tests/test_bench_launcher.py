@@ -30,6 +30,15 @@ def test_plain_gpus2_spawns_two_ranks_under_gloo():
     assert rec['pixels'] == 2 * 3 * 3840 * 2160         # SUM over ranks: each rank's 3-frame shard
     assert rec['max_elapsed_s'] == 0.002                # MAX over ranks (rank r reports 0.001 (r + 1))
     assert rec['gamma'] == 2.2 and rec['lattice_sum'] > 0   # rank 0's params / lattice reached rank 1
+    # the line carries BASELINE's multi-GPU configurations beside C2, each
+    # sharded over both ranks
+    assert rec['config']['workload'].startswith('C2')
+    sh = rec['config']['sharded_configs']
+    assert sh['C4']['workload'].startswith('C4') and 'mobius' in sh['C4']['workload']
+    assert sh['C5']['workload'].startswith('C5') and '7680x4320' in sh['C5']['workload']
+    assert sh['C4']['pixels'] == 2 * 64 * 3840 * 2160 and sh['C4']['frames_total'] == 128
+    assert sh['C5']['pixels'] == 2 * 16 * 7680 * 4320
+    assert sh['C4']['max_elapsed_s'] == 0.002
 
 
 def test_gpus_must_equal_world_size():

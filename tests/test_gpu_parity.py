@@ -597,6 +597,73 @@ def test_concurrent_contexts_on_threads_match_serial():
         c.close()
 
 
+def test_set_params_waits_only_for_its_own_context():
+    """h2s_set_params / h2s_set_lut drain the context's OWN queued launches
+    (events recorded after them), not the device: with
+    a ~0.3 s spin kernel queued on a side stream, ahead of context A's launch
+    on that stream, context B's set_params returns at once, while A's waits
+    for its launch (and so for the spin ahead of it)."""
+    import time
+    import torch
+    W, H = 256, 128
+    p = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2)
+    a = hdr2sdr.Tonemapper(0, p, lattice(65))
+    b = hdr2sdr.Tonemapper(0, p, lattice(65))
+    src = synth_frames('smooth', 2, W, H, 10, device='cpu', seed=4).to_torch('cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(2, W, H, 10, 'cuda')
+    b.process(src, dst)          # b has launched before (its own events drain at once)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    # calibrate torch's spin kernel (its cycle counter's rate) to ~0.3 s
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    torch.cuda._sleep(50_000_000)
+    torch.cuda.synchronize()
+    spin = int(50_000_000 * 0.3 / max(time.perf_counter() - t0, 1e-4))
+    try:
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(spin)
+        a.process(src, dst, side)                       # queued behind the spin
+        t0 = time.perf_counter()
+        b.set_params(p.with_(gamma=1.5))
+        b.set_lut(lattice(33))
+        tb = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        a.set_params(p.with_(gamma=1.5))
+        ta = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        assert tb < 0.1, f'set_params on B waited {tb:.3f} s for work that is not its own'
+        assert ta > 0.1, f'set_params on A returned after {ta:.3f} s, before its queued launch ran'
+    finally:
+        a.close()
+        b.close()
+
+
+def test_two_pass_scratch_serialised_across_streams(tm):
+    """The BICUBIC two-pass path uses one per-context scratch plane: two
+    launches on two streams from the same thread run one after the other
+    (ADVICE r02), so both outputs equal the serial result."""
+    import torch
+    W, H = 512, 256
+    params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, chroma_filter='bicubic')
+    tm.set_params(params)
+    tm.set_lut(lattice(65))
+    s1 = synth_frames('smooth', 3, W, H, 10, device='cpu', seed=61).to_torch('cuda')
+    s2 = synth_frames('uniform', 3, W, H, 10, device='cpu', seed=62).to_torch('cuda')
+    want1, want2 = tm(s1).to_numpy().buf, tm(s2).to_numpy().buf
+    d1 = hdr2sdr.FrameBatch.empty_torch(3, W, H, 10, 'cuda')
+    d2 = hdr2sdr.FrameBatch.empty_torch(3, W, H, 10, 'cuda')
+    st1, st2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        tm.process(s1, d1, st1)
+        tm.process(s2, d2, st2)
+    torch.cuda.synchronize()
+    assert np.array_equal(d1.to_numpy().buf, want1)
+    assert np.array_equal(d2.to_numpy().buf, want2)
+
+
 def test_peak_exchange_and_lp_tone_errors(tm):
     """h2s_peak_stats takes device frames only; h2s_peak_feed rejects
     mismatched arrays; an unknown lp_tone is INVALID_ARG at set_params (the
