@@ -26,7 +26,8 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, u
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
                              int w, int h, uint8_t* rgb, long long rls, const uint8_t* glut, hipStream_t s);
 constexpr int PEAK_BLOCKS = 64;  // partial (max, sum) records per frame
-hipError_t launch_peak_stats(const KParams& P, float2* partial, hipStream_t s);
+constexpr int PEAK_BINS = 1024;  // percentile histogram bins over PQ [0, 1] (h2s_kernels.hip)
+hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s);
 }  // namespace h2s
 
 using h2s::FastParams;
@@ -51,7 +52,6 @@ struct h2s_ctx {
   bool fast_enabled = true;
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
-  int kernel = 0;           // 0: k_tile, 1: k_wave (H2S_KERNEL=tile|wave)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
@@ -83,6 +83,8 @@ struct h2s_ctx {
   hipEvent_t chr_ev = nullptr;   // after the last BICUBIC two-pass launch (d_chr scratch in use)
   bool chr_pending = false;
   float2* d_chr = nullptr;       // BICUBIC chroma: one frame's per-pixel (Cb, Cr)
+  unsigned* d_hist = nullptr;    // peak_detect percentile: per-frame PQ histograms
+  size_t hist_cap = 0;
   size_t chr_cap = 0;
 };
 
@@ -380,9 +382,24 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   const bool lp = k->pipe == h2s::PIPE_LIBPLACEBO;
   k->rgba8 = lp && p->lut_enabled ? 1 : 0;
   k->lp_ipt = lp && p->lp_tone == H2S_LP_TONE_IPT ? 1 : 0;
+  // libplacebo stage options (ABI v3): range=tv on the rgba output, the
+  // download's dither, the 12-bit input through format=p010
+  const bool lim = lp && p->lp_range == H2S_LP_RANGE_LIMITED;
+  k->lp_qs = lim ? 219.0f : 255.0f;
+  k->lp_qo = lim ? 16.0f : 0.0f;
+  k->lp_dith = lp && p->lp_dither == H2S_LP_DITHER_ORDERED ? 1 : 0;
+  k->in_mask = lp && p->lp_p010 == H2S_LP_P010_TRUNCATE && p->bits_in == 12 ? 0xFFFCu : 0xFFFFu;
   ipt_matrices(k->ipt_r2l, k->ipt_l2r);
   k->t_white = isnan(p->target_white) ? (lp ? 203.0 : p->npl) : p->target_white;
   k->t_black = isnan(p->target_black) ? (lp ? k->t_white / 1000.0 : 0.0) : p->target_black;
+  // peak_detect=1: vf_libplacebo's option defaults (smoothing_period 100,
+  // scene_threshold_low / high 5.5 / 10, percentile 99.995, minimum_peak 1
+  // x the SDR white); PARITY UNPINNED
+  k->pd_smoothing = isnan(p->pd_smoothing) ? 100.0 : p->pd_smoothing;
+  k->pd_scene_low = isnan(p->pd_scene_low) ? 5.5 : p->pd_scene_low;
+  k->pd_scene_high = isnan(p->pd_scene_high) ? 10.0 : p->pd_scene_high;
+  k->pd_percentile = isnan(p->pd_percentile) ? 99.995 : p->pd_percentile;
+  k->pd_min = (isnan(p->pd_min_peak) ? 1.0 : p->pd_min_peak) * k->t_white / 100.0;
   k->knee_off = isnan(p->knee_offset) ? 1.0 : p->knee_offset;
   {
     const double lb = pow(k->t_black / k->t_white, 1.0 / 2.4), a = pow(1.0 - lb, 2.4);
@@ -683,7 +700,6 @@ int h2s_create(int device, h2s_ctx** out) {
   c->device = device;
   h2s_params_default(&c->params);
   if (const char* v = getenv("H2S_HOST_SERIAL")) c->serial_host = atoi(v) != 0;
-  if (const char* v = getenv("H2S_KERNEL")) c->kernel = strcmp(v, "wave") == 0 ? 1 : 0;
   if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
     const int tpb = atoi(v);
     if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
@@ -706,6 +722,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_peak) hipFree(c->d_peak);
   if (c->d_curve) hipFree(c->d_curve);
   if (c->d_chr) hipFree(c->d_chr);
+  if (c->d_hist) hipFree(c->d_hist);
   if (c->curve_ev) hipEventDestroy(c->curve_ev);
   if (c->chr_ev) hipEventDestroy(c->chr_ev);
   for (hipEvent_t ev : c->pend) hipEventDestroy(ev);
@@ -916,6 +933,10 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->c56 = 56.0f * k.qscale;
   for (int i = 0; i < 3; i++) F->k709[i] = k.k709[i], F->kcb[i] = k.kcb[i], F->kcr[i] = k.kcr[i];
   F->lp_ipt = k.lp_ipt;
+  F->lp_qs_f = k.lp_qs / 255.0f;
+  F->lp_qo = k.lp_qo;
+  F->lp_dith = k.lp_dith;
+  F->in_mask2 = k.in_mask | (k.in_mask << 16);
   for (int i = 0; i < 9; i++)
     F->ipt_r2l[i] = (float)(k.ipt_r2l[i] * k.ipt_npl), F->ipt_l2r[i] = (float)(k.ipt_l2r[i] * (p->npl / k.t_white));
   F->pqi_tab = c->d_pqi;
@@ -1050,7 +1071,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   }
   // k_tile covers the whole 64-pixel tiles; the chroma right halo of its last
   // tile reads the real column (F.cw stays the frame's), so the split is exact
-  const int tw = c->kernel ? h2s::WTW : h2s::TBW;
+  const int tw = h2s::TBW;
   const int w64 = k.W & ~(tw - 1);
   F.W = w64, F.H = k.H, F.cw = k.cw, F.ch = k.ch;
   F.chroma_edge = k.chroma_edge;
@@ -1059,9 +1080,8 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
     F.in_bytes[p] = (int)(ib < 0x7fffffff ? ib : 0x7fffffff);
     F.out_bytes[p] = (int)(ob < 0x7fffffff ? ob : 0x7fffffff);
   }
-  F.kernel = c->kernel;
   F.nbx = (unsigned)(w64 / tw);
-  F.nby = (unsigned)(c->kernel ? (k.H + h2s::WTH - 1) / h2s::WTH : (k.H + h2s::TBH - 1) / h2s::TBH);
+  F.nby = (unsigned)((k.H + h2s::TBH - 1) / h2s::TBH);
   F.nframes = (unsigned)nframes;
   F.tpb = c->tiles_per_block;
   F.cv_frames = cvf;
@@ -1094,7 +1114,7 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
 
 static int choose_path(const h2s_ctx* c, const KParams& k, const h2s_frames* din, const h2s_frames* dout,
                        bool out8) {
-  const int tw = c->kernel ? h2s::WTW : h2s::TBW;
+  const int tw = h2s::TBW;
   if (fast_params_ok(c, k) && tile_ok(din, dout, out8, tw))
     return (din->width & (tw - 1)) ? H2S_PATH_TILE_TAIL : H2S_PATH_TILE;
   return c->params.chroma_filter == H2S_CHROMA_BICUBIC ? H2S_PATH_TWO_PASS : H2S_PATH_GENERIC;
@@ -1119,11 +1139,19 @@ static int ensure_chr(h2s_ctx* c, const KParams& k) {
 // average, bypassed progressively for scene changes whose average moves by
 // 10..30 % PQ (smoothstep); the result is clamped to [1, static peak].
 static double peak_update(h2s_ctx* c, double fmax, double favg, double static_peak) {
+  const KParams& k = c->k;
   if (c->pk_frames == 0) {
     c->pk_max = fmax, c->pk_avg = favg;
   } else {
-    const double a = 1.0 - exp(-1.0 / 20.0);
-    double t = (fabs(favg - c->pk_avg) * 100.0 - 10.0) / 20.0;
+    // IIR with coefficient 1 - exp(-1 / smoothing_period); a scene change
+    // (frame-average jump of scene_low .. scene_high % PQ) bypasses it
+    // progressively (smoothstep); negative thresholds turn that off
+    const double a = k.pd_smoothing > 0.0 ? 1.0 - exp(-1.0 / k.pd_smoothing) : 1.0;
+    const double d = fabs(favg - c->pk_avg) * 100.0;
+    double t = 0.0;
+    if (k.pd_scene_low >= 0.0 && k.pd_scene_high >= 0.0)
+      t = k.pd_scene_high > k.pd_scene_low ? (d - k.pd_scene_low) / (k.pd_scene_high - k.pd_scene_low)
+                                           : (d >= k.pd_scene_low ? 1.0 : 0.0);
     t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
     const double w = a + (1.0 - a) * t * t * (3.0 - 2.0 * t);
     c->pk_max += w * (fmax - c->pk_max);
@@ -1131,7 +1159,7 @@ static double peak_update(h2s_ctx* c, double fmax, double favg, double static_pe
   }
   c->pk_frames++;
   double peak = pq_eotf_d(c->pk_max) * 100.0;  // units of 100 nits, as vf_tonemap's peak
-  if (peak < 1.0) peak = 1.0;
+  if (peak < k.pd_min) peak = k.pd_min;          // minimum_peak x the target white
   if (peak > static_peak) peak = static_peak;
   c->pk_peak = peak;
   return peak;
@@ -1144,6 +1172,26 @@ static double peak_update(h2s_ctx* c, double fmax, double favg, double static_pe
 // ragged tail columns go frame by frame.
 // per-frame max and mean of the PQ-encoded max(R,G,B) for the batch k binds
 // (k_peak_stats_v partials, folded on the host)
+// the pct-th percentile of a frame's PQ(max R,G,B) from its histogram
+// (bins of 1/nb over [0, 1]): the first bin whose cumulative count reaches
+// pct % of the pixels, interpolated linearly inside it, capped at the frame
+// maximum (oracle_peak_stats; PARITY UNPINNED: libplacebo's own histogram
+// and interpolation are not restated)
+static double pq_percentile(const unsigned* h, int nb, double pct, double mx) {
+  double n = 0.0;
+  for (int i = 0; i < nb; i++) n += h[i];
+  const double target = pct / 100.0 * n;
+  double cum = 0.0;
+  for (int i = 0; i < nb; i++) {
+    if (h[i] && cum + h[i] >= target) {
+      const double v = (i + (target - cum) / h[i]) / nb;
+      return v < mx ? v : mx;
+    }
+    cum += h[i];
+  }
+  return mx;
+}
+
 static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, std::vector<double>* fmax,
                        std::vector<double>* favg) {
   const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
@@ -1157,9 +1205,26 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
     }
     c->peak_cap = need;
   }
-  hipError_t e = h2s::launch_peak_stats(k, c->d_peak, s);
+  // pd_percentile < 100: a per-frame histogram of PQ(max R,G,B) as well
+  const bool pct = k.pd_percentile < 100.0;
+  const size_t hneed = pct ? (size_t)nframes * h2s::PEAK_BINS : 0;
+  if (hneed > c->hist_cap) {
+    if (c->d_hist) hipFree(c->d_hist);
+    c->d_hist = nullptr;
+    c->hist_cap = 0;
+    if (hipMalloc((void**)&c->d_hist, hneed * sizeof(unsigned)) != hipSuccess) {
+      c->d_hist = nullptr;
+      return fail(c, H2S_E_OOM, "peak histogram allocation failed");
+    }
+    c->hist_cap = hneed;
+  }
+  hipError_t e = pct ? hipMemsetAsync(c->d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
+  if (e == hipSuccess) e = h2s::launch_peak_stats(k, c->d_peak, pct ? c->d_hist : nullptr, s);
   std::vector<float2> part(need);
+  std::vector<unsigned> hist(hneed);
   if (e == hipSuccess) e = hipMemcpyAsync(part.data(), c->d_peak, need * sizeof(float2), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && pct)
+    e = hipMemcpyAsync(hist.data(), c->d_hist, hneed * sizeof(unsigned), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
   const double npx = (double)k.W * k.H;
@@ -1172,7 +1237,7 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
       mx = v.x > mx ? v.x : mx;
       sum += v.y;
     }
-    (*fmax)[f] = mx;
+    (*fmax)[f] = pct ? pq_percentile(&hist[(size_t)f * h2s::PEAK_BINS], h2s::PEAK_BINS, k.pd_percentile, mx) : mx;
     (*favg)[f] = sum / npx;
   }
   return 0;
@@ -1222,10 +1287,10 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
     if (e == hipSuccess) e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
     if (e == hipSuccess) e = hipEventRecord(c->curve_ev, s);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
-    if ((k.W & ((c->kernel ? h2s::WTW : h2s::TBW) - 1)) == 0) return 0;
+    if ((k.W & (h2s::TBW - 1)) == 0) return 0;
   }
   for (int f = 0; f < nframes; f++) {
-    e = fast ? launch_tail(kfs[f], 1, vec, out8, s, c->kernel ? h2s::WTW : h2s::TBW) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
+    e = fast ? launch_tail(kfs[f], 1, vec, out8, s, h2s::TBW) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   }
   return 0;

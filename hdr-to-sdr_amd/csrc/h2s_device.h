@@ -49,6 +49,16 @@ struct KParams {
   int pipe, rgba8;
   float enc_ainv, enc_b;  // libplacebo BT.1886 encode: (x * ainv)^(1/2.4) - b
   int lp_ipt;             // libplacebo branch: the curve on IPT-PQ intensity (h2s_lp_tone IPT)
+  // libplacebo branch options (include/h2s.h ABI v3): rgba8 code =
+  // floor(clamp01(v) lp_qs + lp_qo + (lp_dith ? bayer16(x, y) : 0.5));
+  // in_mask: input code mask (0xFFFC: a 12-bit input through format=p010
+  // with the two low bits dropped, h2s_lp_p010 TRUNCATE)
+  float lp_qs, lp_qo;
+  int lp_dith;
+  unsigned in_mask;
+  // peak_detect (host side): IIR period (frames), scene thresholds (% PQ),
+  // percentile, minimum peak (units of 100 nits)
+  double pd_smoothing, pd_scene_low, pd_scene_high, pd_percentile, pd_min;
   double ipt_r2l[9], ipt_l2r[9];  // BT.2020 RGB -> LMS (HPE), inverse (row-major)
   double ipt_npl, ipt_os;         // npl / 10000, 10000 / target white (double)
   // libplacebo reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = target white)
@@ -113,7 +123,6 @@ struct FastParams : CurveConsts {
   int chroma_edge;                 // S1 upsampler edge rule (chroma_edge_at)
   unsigned nbx, nby, nframes;      // 64 x 32 tiles per row / column, frames
   int tpb;                         // tiles walked by one block (k_tile prefetches tile i+1 during tile i)
-  int kernel;                      // 0: k_tile (64 x 32 tiles per block), 1: k_wave (32 x 16 tiles per wave)
   const uint8_t* in[3];
   long long in_ls[3], in_fp[3];
   uint8_t* out[3];
@@ -141,6 +150,12 @@ struct FastParams : CurveConsts {
   // lp_tone = IPT: RGB (npl units) -> LMS / 10000 (npl/10000 folded in); LMS
   // -> RGB; the PQ encode as PQI_NSEG cubic segments (pqi)
   int lp_ipt;
+  // rgba8 download (the LP instances): code = floor(e lp_qs_f + qoff), e the
+  // 255-scaled encode, qoff = lp_qo + (lp_dith ? bayer16 : 0.5) per pixel;
+  // in_mask2: the input code mask on a packed pair of samples
+  float lp_qs_f, lp_qo;
+  int lp_dith;
+  unsigned in_mask2;
   float ipt_r2l[9], ipt_l2r[9];
   const float4* pqi_tab;
   // libplacebo branch with the LUT off (k_tile<..., LP = 1>): libplacebo's own
@@ -173,7 +188,6 @@ struct FastParams : CurveConsts {
 };
 
 constexpr int TBW = 64, TBH = 32;   // k_tile: luma tile of one block
-constexpr int WTW = 32, WTH = 16;   // k_wave: luma tile of one wave
 constexpr int PQ_SEG = 128;          // segments per unit of E
 constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
 constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
@@ -435,12 +449,32 @@ __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
 // libplacebo branch: rgba8 download (round to nearest), then vf_lut3d's 8-bit
 // path: coordinate clip((q / 255) (N-1)), tetrahedral, output truncated to
 // 8 bits; returns the 8-bit values / 255
-__device__ __forceinline__ float rgba8_q(float v) { return floorf(clamp01(v) * 255.0f + 0.5f); }
+// qoff: lp_qoff (the range=tv offset and the rounding / dither offset)
+__device__ __forceinline__ float rgba8_q(const KParams& P, float v, float qoff) {
+  return floorf(fmaf(clamp01(v), P.lp_qs, qoff));
+}
 
-__device__ __forceinline__ void lut3d_8bit(const KParams& P, float& r, float& g, float& b) {
+// 16 x 16 Bayer matrix (M_2n = 4 M_n + M_1 per 2 x 2 block, M_1 = [0 2; 3 1])
+// as a dither offset (M + 0.5) / 256 in (0, 1): the h2s_lp_dither ORDERED model
+__host__ __device__ __forceinline__ float bayer16(int x, int y) {
+  int m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int bx = (x >> i) & 1, by = (y >> i) & 1;
+    m += (2 * (bx ^ by) + by) << (2 * (3 - i));
+  }
+  return ((float)m + 0.5f) * (1.0f / 256.0f);
+}
+
+// the rgba8 download's offset for pixel (x, y)
+__device__ __forceinline__ float lp_qoff(const KParams& P, int x, int y) {
+  return P.lp_qo + (P.lp_dith ? bayer16(x, y) : 0.5f);
+}
+
+__device__ __forceinline__ void lut3d_8bit(const KParams& P, float& r, float& g, float& b, float qoff) {
   const float sf = 1.0f / 255.0f;
   // lut3d_tetra multiplies by lut_max and clips; (q * 1/255) is its input
-  r = rgba8_q(r) * sf, g = rgba8_q(g) * sf, b = rgba8_q(b) * sf;
+  r = rgba8_q(P, r, qoff) * sf, g = rgba8_q(P, g, qoff) * sf, b = rgba8_q(P, b, qoff) * sf;
   lut3d_tetra(P, r, g, b);
   const float R = fminf(fmaxf(truncf(r * 255.0f), 0.0f), 255.0f);
   const float G = fminf(fmaxf(truncf(g * 255.0f), 0.0f), 255.0f);
@@ -466,7 +500,7 @@ __device__ __forceinline__ void lut3d_16bit(const KParams& P, float& r, float& g
 // S1 (after upsampling) .. S4 on one pixel.  UPTO = last stage to apply.
 template <int UPTO>
 __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, float cr, float& r, float& g,
-                                         float& b) {
+                                         float& b, float qoff = 0.5f) {
   float er = y + P.m_rcr * cr;
   float eg = y + P.m_gcb * cb + P.m_gcr * cr;
   float eb = y + P.m_bcb * cb;
@@ -487,7 +521,7 @@ __device__ __forceinline__ void chain_px(const KParams& P, float y, float cb, fl
     if (P.lut_enabled) {
       r = lp_encode(P, r), g = lp_encode(P, g), b = lp_encode(P, b);
       if (UPTO == 3) return;
-      lut3d_8bit(P, r, g, b);
+      lut3d_8bit(P, r, g, b, qoff);
     } else {
       float mr = P.m709[0] * r + P.m709[1] * g + P.m709[2] * b;
       float mg = P.m709[3] * r + P.m709[4] * g + P.m709[5] * b;

@@ -43,9 +43,7 @@ bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
   if (nt == 0) return hipSuccess;
-  // k_tile: tpb tiles per block; k_wave: tpb groups of 4 tiles (one per wave)
-  const long long per = F.kernel ? 4LL * F.tpb : F.tpb;
-  const long long nb = (nt + per - 1) / per;
+  const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb);
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8 || lp) desat = 0;

@@ -55,8 +55,11 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
       const uint2 a = *reinterpret_cast<const uint2*>(ru + 2 * cx0);
       const uint2 b = *reinterpret_cast<const uint2*>(rv + 2 * cx0);
       const int hx = edge(P, cx0 + 4, cw);
-      int su[5] = {(int)(a.x & 0xffff), (int)(a.x >> 16), (int)(a.y & 0xffff), (int)(a.y >> 16), ld16(ru, hx)};
-      int sv[5] = {(int)(b.x & 0xffff), (int)(b.x >> 16), (int)(b.y & 0xffff), (int)(b.y >> 16), ld16(rv, hx)};
+      const int m = (int)P.in_mask;   // h2s_lp_p010 TRUNCATE drops the two low bits
+      int su[5] = {(int)(a.x & 0xffff) & m, (int)(a.x >> 16) & m, (int)(a.y & 0xffff) & m, (int)(a.y >> 16) & m,
+                   ld16(ru, hx) & m};
+      int sv[5] = {(int)(b.x & 0xffff) & m, (int)(b.x >> 16) & m, (int)(b.y & 0xffff) & m, (int)(b.y >> 16) & m,
+                   ld16(rv, hx) & m};
 #pragma unroll
       for (int k = 0; k <= QPT; k++) {
         cu[i][k] = (float)su[k] * P.c_scale + P.c_off;
@@ -66,8 +69,8 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
 #pragma unroll
       for (int k = 0; k <= QPT; k++) {
         const int x = edge(P, cx0 + k, cw);
-        cu[i][k] = (float)ld16(ru, x) * P.c_scale + P.c_off;
-        cv[i][k] = (float)ld16(rv, x) * P.c_scale + P.c_off;
+        cu[i][k] = (float)(ld16(ru, x) & (int)P.in_mask) * P.c_scale + P.c_off;
+        cv[i][k] = (float)(ld16(rv, x) & (int)P.in_mask) * P.c_scale + P.c_off;
       }
     }
   }
@@ -94,14 +97,14 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
       const unsigned w[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        ys[j][2 * k] = (int)(w[k] & 0xffff);
-        ys[j][2 * k + 1] = (int)(w[k] >> 16);
+        ys[j][2 * k] = (int)(w[k] & 0xffff & P.in_mask);
+        ys[j][2 * k + 1] = (int)((w[k] >> 16) & P.in_mask);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 2 * QPT; k++) {
         const int x = x0 + k < P.W ? x0 + k : P.W - 1;
-        ys[j][k] = ld16(ry, x);
+        ys[j][k] = ld16(ry, x) & (int)P.in_mask;
       }
     }
   }
@@ -118,12 +121,12 @@ __global__ __launch_bounds__(256) void k_process(const KParams P) {
       const float cr = j == 0 ? 0.25f * hv[0][x] + 0.75f * hv[1][x] : 0.75f * hv[1][x] + 0.25f * hv[2][x];
       const float yv = (float)ys[j][x] * P.y_scale + P.y_off;
       float r, g, b;
-      chain_px<4>(P, yv, cb, cr, r, g, b);
+      const int px = 2 * (cx0 + k) + (p & 1), py = 2 * cy + j;
+      chain_px<4>(P, yv, cb, cr, r, g, b, lp_qoff(P, px, py));
       r = clamp01(r), g = clamp01(g), b = clamp01(b);
       const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
       cbs[p] = P.kcb[0] * r + P.kcb[1] * g + P.kcb[2] * b;
       crs[p] = P.kcr[0] * r + P.kcr[1] * g + P.kcr[2] * b;
-      const int px = 2 * (cx0 + k) + (p & 1), py = 2 * cy + j;
       int yq = quant_o((16.0f + 219.0f * Y) * P.qscale, P.dither ? dither_off(px, py) : 0.5f, P.qmax);
       if (!P.eq_identity) yq = P.eq_lut[yq];
       yo[j][x] = expand_code(P, yq);
@@ -211,9 +214,9 @@ __global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
   auto hpass = [&](int plane, int cyy) -> float {
     const uint8_t* row = P.in[plane] + edge(P, cyy, ch) * P.in_ls[plane];
     const int k = x >> 1;
-    const float a = (float)ld16(row, edge(P, k, cw)) * P.c_scale + P.c_off;
+    const float a = (float)(ld16(row, edge(P, k, cw)) & (int)P.in_mask) * P.c_scale + P.c_off;
     if (!(x & 1)) return a;
-    const float b = (float)ld16(row, edge(P, k + 1, cw)) * P.c_scale + P.c_off;
+    const float b = (float)(ld16(row, edge(P, k + 1, cw)) & (int)P.in_mask) * P.c_scale + P.c_off;
     return 0.5f * a + 0.5f * b;
   };
   auto up = [&](int plane) -> float {
@@ -222,9 +225,9 @@ __global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
     return 0.75f * hpass(plane, m) + 0.25f * hpass(plane, m + 1);
   };
   const float cb = up(1), cr = up(2);
-  const float yv = (float)ld16(P.in[0] + y * P.in_ls[0], x) * P.y_scale + P.y_off;
+  const float yv = (float)(ld16(P.in[0] + y * P.in_ls[0], x) & (int)P.in_mask) * P.y_scale + P.y_off;
   float r, g, b;
-  chain_px<STAGE < 5 ? STAGE : 4>(P, yv, cb, cr, r, g, b);
+  chain_px<STAGE < 5 ? STAGE : 4>(P, yv, cb, cr, r, g, b, lp_qoff(P, x, y));
   if (STAGE == 5) {  // S6 quantiser inputs (oracle px_yuv)
     r = clamp01(r), g = clamp01(g), b = clamp01(b);
     const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
@@ -332,6 +335,7 @@ hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8,
 // one pixel's PQ-domain max(R,G,B) from its integer codes (nearest chroma)
 template <int TRC>
 __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned uc, unsigned vc) {
+  yc &= P.in_mask, uc &= P.in_mask, vc &= P.in_mask;
   const float Y = (float)yc * P.y_scale + P.y_off;
   const float cb = (float)uc * P.c_scale + P.c_off, cr = (float)vc * P.c_scale + P.c_off;
   const float er = Y + P.m_rcr * cr, eg = Y + P.m_gcb * cb + P.m_gcr * cr, eb = Y + P.m_bcb * cb;
@@ -340,6 +344,19 @@ __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned
   const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * bl;
   const float w = ys > 0.0f ? P.lin_scale * apow(ys, 0.2f) : 0.0f;
   return clamp01(pq_encode(fmaxf(fmaxf(r, g), bl) * w * P.npl_1e4));
+}
+
+// percentile model (pd_percentile < 100; PARITY UNPINNED):
+// a PEAK_BINS-bin histogram of the per-pixel PQ(max R,G,B) per frame; the
+// host interpolates the percentile inside its bin (oracle_peak_stats)
+constexpr int PEAK_BINS = 1024;
+__device__ __forceinline__ void hist_add(unsigned* lh, float m) {
+  atomicAdd(&lh[min((int)(m * (float)PEAK_BINS), PEAK_BINS - 1)], 1u);
+}
+__device__ __forceinline__ void hist_flush(const unsigned* lh, unsigned* hist) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < PEAK_BINS; i += 256)
+    if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
 
 // block (max, sum) reduction; thread 0 writes the record
@@ -358,8 +375,12 @@ __device__ __forceinline__ void peak_reduce(float mx, float sm, float2* out) {
 }
 
 // generic form: any width / alignment, 2-byte loads
-template <int TRC>
-__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial) {
+template <int TRC, bool HIST>
+__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial, unsigned* hist) {
+  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (HIST)
+    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
+  if (HIST) __syncthreads();
   const int f = blockIdx.y, b = blockIdx.x;
   float mx = 0.0f, sm = 0.0f;
   for (int y = b; y < P.H; y += gridDim.x) {
@@ -371,17 +392,23 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
       const float m = peak_px<TRC>(P, yr[x], ur[x >> 1], vr[x >> 1]);
       mx = fmaxf(mx, m);
       rs += m;
+      if (HIST) hist_add(lh, m);
     }
     sm += rs;
   }
+  if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
   peak_reduce(mx, sm, &partial[f * gridDim.x + b]);
 }
 
 // streaming form (W % 8 == 0, 16-byte luma / 8-byte chroma alignment): each
 // thread takes 8-pixel chunks (one 16-byte luma load, one 8-byte load per
 // chroma plane), two chunks per iteration so two loads per plane are in flight
-template <int TRC>
-__global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial) {
+template <int TRC, bool HIST>
+__global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, unsigned* hist) {
+  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (HIST)
+    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
+  if (HIST) __syncthreads();
   const int f = blockIdx.y;
   const int cpr = P.W >> 3;                       // chunks per row
   const int nch = P.H * cpr, stride = gridDim.x * 256;
@@ -406,6 +433,7 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
       const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
       mx = fmaxf(mx, m);
       rs += m;
+      if (HIST) hist_add(lh, m);
     }
     sm += rs;
   };
@@ -424,25 +452,34 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
     chunk(i, ya, ua, va);
     fold(ya, ua, va);
   }
+  if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
   peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
 }
 
 constexpr int PEAK_BLOCKS_K = 64;
-hipError_t launch_peak_stats(const KParams& P, float2* partial, hipStream_t s) {
+// hist: nframes x PEAK_BINS zeroed counters (the percentile model), or null
+hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s) {
   const dim3 grid(PEAK_BLOCKS_K, P.nframes);
   auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
   const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
                    al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
                    al(P.in_fp[1], 8) && al((long long)(uintptr_t)P.in[2], 8) && al(P.in_ls[2], 8) &&
                    al(P.in_fp[2], 8);
-  if (vec && P.transfer == 1)
-    hipLaunchKernelGGL(k_peak_stats_v<1>, grid, dim3(256), 0, s, P, partial);
-  else if (vec)
-    hipLaunchKernelGGL(k_peak_stats_v<0>, grid, dim3(256), 0, s, P, partial);
-  else if (P.transfer == 1)
-    hipLaunchKernelGGL(k_peak_stats<1>, grid, dim3(256), 0, s, P, partial);
-  else
-    hipLaunchKernelGGL(k_peak_stats<0>, grid, dim3(256), 0, s, P, partial);
+#define H2S_PEAK_LAUNCH(HI)                                                                   \
+  if (vec && P.transfer == 1)                                                                 \
+    hipLaunchKernelGGL((k_peak_stats_v<1, HI>), grid, dim3(256), 0, s, P, partial, hist);     \
+  else if (vec)                                                                               \
+    hipLaunchKernelGGL((k_peak_stats_v<0, HI>), grid, dim3(256), 0, s, P, partial, hist);     \
+  else if (P.transfer == 1)                                                                   \
+    hipLaunchKernelGGL((k_peak_stats<1, HI>), grid, dim3(256), 0, s, P, partial, hist);       \
+  else                                                                                        \
+    hipLaunchKernelGGL((k_peak_stats<0, HI>), grid, dim3(256), 0, s, P, partial, hist);
+  if (hist) {
+    H2S_PEAK_LAUNCH(true)
+  } else {
+    H2S_PEAK_LAUNCH(false)
+  }
+#undef H2S_PEAK_LAUNCH
   return hipGetLastError();
 }
 

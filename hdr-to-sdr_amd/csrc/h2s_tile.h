@@ -27,8 +27,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "h2s_device.h"
 
 namespace h2s {
@@ -351,7 +349,7 @@ template <int TRC, int TM, int DESAT, int LP, int DBG>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv) {
+                                             long long di, float& oyv, float& ozv, float qoff = 0.5f) {
   constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
@@ -385,13 +383,14 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   } else {
     float sr, sg, sb;
     if (LP) {
-      // 255 (BT.1886 encode) rounded to the 8-bit rgba code, then lut3d's
-      // 8-bit coordinate (q / 255) (N-1) in its own operation order: q = 255
-      // lands on N-1 exactly (fract 0: the corners past the lattice edge
-      // get weight 0 and read in-bounds records or the buffer's zero fill)
+      // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the
+      // range=tv and rounding / dither offsets, h2s_lp_range / _dither), then
+      // lut3d's 8-bit coordinate (q / 255) (N-1) in its own operation order:
+      // q = 255 lands on N-1 exactly (fract 0: the corners past the lattice
+      // edge get weight 0 and read in-bounds records or the buffer's zero fill)
       auto q8 = [&](float x) -> float {
         const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        return floorf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) + 0.5f);
+        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
       };
       const float qr = q8(r), qg = q8(gg), qb = q8(bl);
       if (DBG == 3) {
@@ -660,9 +659,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
   const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max};
+  // libplacebo branch: the rgba8 download offset of this lane's pixel at step
+  // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
+  // origins are multiples of 16)
+  float qo[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    qo[i] = LP ? F.lp_qo + (F.lp_dith ? bayer16(xl + 8 * (i & 1), yl + 8 * (i >> 1)) : 0.5f) : 0.5f;
 
   for (;;) {
     // ---- commit this tile's registers to LDS ----
+    if (F.in_mask2 != 0xFFFFFFFFu) {   // h2s_lp_p010 TRUNCATE (block-uniform)
+      cur.ya.x &= F.in_mask2, cur.ya.y &= F.in_mask2, cur.ya.z &= F.in_mask2, cur.ya.w &= F.in_mask2;
+      cur.ua.x &= F.in_mask2, cur.ua.y &= F.in_mask2, cur.ua.z &= F.in_mask2, cur.ua.w &= F.in_mask2;
+      cur.uh &= F.in_mask2;
+    }
     {
       float v[8];
       unpack8(cur.ya, v);
@@ -713,8 +724,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                                : -1;
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
-      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] =
-          px_chain<TRC, TM, DESAT, LP, DBG>(F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv);
+      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG>(
+          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f);
       const f3 o = {0.0f, oyv, ozv};
       // chroma: 2x2 sums; the 4 lanes of a quad store the same value
       const float su = quad_sum(o.y), sv = quad_sum(o.z);
@@ -772,282 +783,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 }
 
 
-// ---------------------------------------------------------------------------
-// k_wave: the same chain with one 32 x 16 luma tile per WAVE (8 dense 8 x 8
-// steps, one pixel per lane as k_tile) and no workgroup barrier after the
-// table staging: each wave stages its own tile in its own LDS slice, so the
-// four waves of a block (and the 20 of a CU) run their load / compute / store
-// phases independently instead of in lock step.  Wave w of block b walks the
-// tiles 4 (b tpb + i) + w, i < tpb: the block's waves work on four
-// horizontally adjacent tiles at a time (one 128-pixel luma row segment, one
-// 64-sample chroma row segment: whole 128-byte lines between them).
-constexpr int WCW = 16, WCH = 8;   // its chroma tile
-constexpr int WYST = 40;           // LDS row strides (floats): 4 rows x 8 lanes per half-wave hit 32 banks
-constexpr int WHST = 40;
-
-struct WaveLds {
-  float yin[WTH * WYST];             // luma samples x ys; output codes overwrite them in place
-  float hrow[2][(WCH + 2) * WHST];   // chroma rows (1-row halo) upsampled x2 horizontally
-  float csum[2][WCH * WCW];          // per chroma sample: sum of its 2x2 pixel contributions
-};
-
-struct WRegs {
-  uint4 ya, ua;   // luma chunk; chroma chunk (threads < 40: U rows on 0..19, V rows on 20..39)
-  unsigned uh;    // the chroma chunk's right-halo sample
-};
-
-struct WGeo {
-  int f, px0, py0, cx0, cy0;
-};
-
-__device__ __forceinline__ WGeo wtile_geo(const FastParams& F, unsigned tile) {
-  const unsigned tx = tile % F.nbx, bt = tile / F.nbx;
-  WGeo g;
-  g.f = (int)(bt / F.nby);
-  const int ty = (int)(bt % F.nby);
-  g.px0 = (int)tx * WTW, g.py0 = ty * WTH, g.cx0 = (int)tx * WCW, g.cy0 = ty * WCH;
-  return g;
-}
-
-// per-lane byte offsets relative to a tile origin (launch constants)
-struct WLaneOfs {
-  int y, u;     // loads: luma row t/4, chunk t%4; chroma row tc/2, chunk tc%2 (tc = t mod 20)
-  int sy, sc;   // stores: luma row t/4, chunk t%4; chroma row (t%16)/2, chunk t%2 of plane t/16
-};
-
-__device__ __forceinline__ WLaneOfs wlane_ofs(const FastParams& F, int t) {
-  WLaneOfs L;
-  L.y = (t >> 2) * (int)F.in_ls[0] + 16 * (t & 3);
-  const int pc = t >= 20, tc = pc ? t - 20 : t;
-  L.u = (tc >> 1) * (int)F.in_ls[1 + pc] + 16 * (tc & 1);
-  const int sb = F.out8 ? 8 : 16;
-  L.sy = (t >> 2) * (int)F.out_ls[0] + sb * (t & 3);
-  const int pl = (t >> 4) & 1, rem = t & 15;
-  L.sc = (rem >> 1) * (int)F.out_ls[1 + pl] + sb * (rem & 1);
-  return L;
-}
-
-// one plane's chroma chunk (rows cy0-1 .. cy0+8, 2 chunks of 8 samples + the
-// next sample); interior tiles use the lane offset + a scalar origin
-template <int PC>
-__device__ __forceinline__ void wchroma_load(const FastParams& F, const WGeo& g, int tc, int lofs, WRegs& r) {
-  const __amdgpu_buffer_rsrc_t ic = plane_rsrc(F.in[1 + PC] + g.f * F.in_fp[1 + PC], F.in_bytes[1 + PC]);
-  const int ls = (int)F.in_ls[1 + PC];
-  if (g.cy0 >= 1 && g.cy0 + WCH + 1 <= F.ch && g.cx0 + WCW + 1 <= F.cw) {   // wave-uniform
-    const int so = (g.cy0 - 1) * ls + 2 * g.cx0;
-    r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, lofs, so, NT));
-    r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, lofs + 16, so, 0);
-  } else {
-    const int clr = tc >> 1, ccx = tc & 1;
-    const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
-    const int hx = 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
-    r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, row * ls + 2 * (g.cx0 + 8 * ccx), 0, NT));
-    r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, row * ls + hx, 0, 0);
-  }
-}
-
-__device__ __forceinline__ WRegs wtile_load(const FastParams& F, const WGeo& g, int t, const WLaneOfs& L) {
-  const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], F.in_bytes[0]);
-  WRegs r;
-  if (g.py0 + WTH <= F.H)   // wave-uniform
-    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                         iy, L.y, g.py0 * (int)F.in_ls[0] + 2 * g.px0, NT));
-  else
-    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-        iy, (g.py0 + (t >> 2) < F.H ? g.py0 + (t >> 2) : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * (t & 3)), 0, NT));
-  if (t < 20)
-    wchroma_load<0>(F, g, t, L.u, r);
-  else if (t < 40)
-    wchroma_load<1>(F, g, t - 20, L.u, r);
-  return r;
-}
-
-template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_wave(const FastParams F) {
-  __shared__ WaveLds wls[4];
-  __shared__ float4 pq_lds[(TRC == 0 || LP) ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
-  __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
-  extern __shared__ uint16_t eq_lds[];                            // eq table, codes pre-shifted to the output depth
-  constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
-
-  const int t = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const unsigned ntiles = F.nbx * F.nby * F.nframes;
-  unsigned q = (unsigned)fxcd_remap(blockIdx.x, gridDim.x) * (unsigned)F.tpb;
-  const unsigned qend = q + (unsigned)F.tpb;
-  unsigned tile = 4 * q + (unsigned)w;
-
-  // ---- prologue: tables (the kernel's one workgroup barrier) + first tile ----
-  const WLaneOfs lofs = wlane_ofs(F, t);
-  WGeo geo = wtile_geo(F, tile < ntiles ? tile : 0);
-  WRegs cur = wtile_load(F, geo, t, lofs);
-  {
-    const int tt = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
-    const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * tt, 0, 0);  // out of range -> 0
-    float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const bool stage_pq = TRC == 0 || (LP && F.lp_ipt);   // block-uniform
-    if (stage_pq && tt < PQ_NSEG) {
-      const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
-      pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * tt, 0, 0));
-    }
-    if (tt < F.eq_n) eq_lds[tt] = (uint16_t)(eq0 << F.shift_out);
-    for (int i = tt + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
-      eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
-    if (stage_pq && tt < PQ_NSEG) pq_lds[tt + 1] = pq0;
-    if (stage_pq && tt == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (LP && F.lp_ipt) {
-      const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
-      for (int i = tt; i < PQI_NSEG; i += 256)
-        pqi_lds[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpi, 16 * i, 0, 0));
-    }
-  }
-  __syncthreads();
-  if (tile >= ntiles) return;   // (after the barrier: every wave took part in it)
-
-  WaveLds& L = wls[w];
-  // ---- per-lane step geometry: step s -> 8x8 sub-block (s&3, s>>2) of the
-  // 32 x 16 tile; lane = pixel (quad q = lane>>2 in a 4x4 quad grid, position
-  // lane&3 in the quad) ----
-  const int qx = (t >> 2) & 3, qy = t >> 4, pxl = t & 1, pyl = (t >> 1) & 1;
-  const int xl = 2 * qx + pxl, yl = 2 * qy + pyl;     // step (0,0) pixel
-  const float* ybase = L.yin + yl * WYST + xl;
-  // vertical pass (centre siting): 3 x row cy + row cy-1 (top) / cy+1 (bottom)
-  const float* h0 = L.hrow[0] + (qy + 1) * WHST + xl;
-  const float* h1 = L.hrow[1] + (qy + 1) * WHST + xl;
-  const int hb = pyl ? WHST : -WHST;
-  float* csb = L.csum[0] + qy * WCW + qx;
-
-  const float yoff = in_vgpr(F.y_off_c) * (float)ESC + (TRC == 0 ? 1.0f : 0.0f);
-  const float cmid = in_vgpr(F.c_mid);
-  const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
-  const StepK K{in_vgpr(F.a_rv[1]) * (float)ESC, in_vgpr(F.a_gv[1]) * (float)ESC, in_vgpr(F.a_gu[1]) * (float)ESC,
-                in_vgpr(F.a_bu[1]) * (float)ESC, in_vgpr(F.stride_g), in_vgpr(F.stride_b), in_vgpr(F.og),
-                in_vgpr(F.ob), in_vgpr(F.cr), in_vgpr(F.cg), in_vgpr(F.cb), in_vgpr(F.log2_nm1), in_vgpr(F.x_max)};
-
-  for (;;) {
-    // ---- commit this tile's registers to the wave's LDS slice ----
-    {
-      float v[8];
-      unpack8(cur.ya, v);
-      float* d = L.yin + (t >> 2) * WYST + 8 * (t & 3);
-      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
-      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
-    }
-    if (t < 40) {
-      // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
-      // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float
-      float v[9];
-      unpack8(cur.ua, v);
-      v[8] = (float)cur.uh;
-#pragma unroll
-      for (int k = 0; k < 9; k++) v[k] -= cmid;
-      const int pc = t >= 20, tc = pc ? t - 20 : t;
-      float* d = L.hrow[pc] + (tc >> 1) * WHST + 16 * (tc & 1);
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        *reinterpret_cast<float4*>(d + 4 * k) =
-            make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
-    }
-    const WGeo g = geo;
-    CurveConsts cv = F;
-    if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
-    const unsigned nq = q + 1;
-    const bool more = nq < qend && 4 * nq + (unsigned)w < ntiles;   // wave-uniform
-    if (more) {
-      geo = wtile_geo(F, 4 * nq + (unsigned)w);
-      cur = wtile_load(F, geo, t, lofs);  // in flight during this tile's compute
-    }
-    // the wave's own LDS writes above are read by other lanes below: LDS
-    // executes one wave's instructions in order; keep the compiler from
-    // reordering across the phase boundary
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int bx = s & 3, by = s >> 2;
-      const int oy = 8 * by * WYST + 8 * bx;   // compile-time LDS offsets
-      const int oh = 4 * by * WHST + 8 * bx;
-      const int oc = 4 * by * WCW + 4 * bx;
-      const float ybs = ybase[oy];
-      const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
-      const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
-      const long long di = DBG && g.f == 0 && g.py0 + yl + 8 * by < F.H
-                               ? (long long)(g.py0 + yl + 8 * by) * F.dbg_w + g.px0 + xl + 8 * bx
-                               : -1;
-      float oyv, ozv;
-      // luma code (eq applied, shifted) replaces the luma sample this lane read
-      reinterpret_cast<unsigned*>(L.yin)[yl * WYST + xl + oy] =
-          px_chain<TRC, TM, DESAT, LP, DBG>(F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv);
-      // chroma: 2x2 sums; the 4 lanes of a quad store the same value
-      const float su = quad_sum(oyv), sv = quad_sum(ozv);
-      csb[oc] = su;
-      csb[oc + WCH * WCW] = sv;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
-    {
-      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
-      const int r = t >> 2, c = t & 3;
-      if (g.py0 + r < F.H) {
-        const unsigned* src = reinterpret_cast<const unsigned*>(L.yin) + r * WYST + 8 * c;
-        const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
-        const int so = g.py0 * (int)F.out_ls[0];
-        if (F.out8)
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
-              oy_, lofs.sy, so + g.px0, NT);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
-              oy_, lofs.sy, so + 2 * g.px0, NT);
-      }
-    }
-    if (t < 32) {
-      // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
-      const int pl = t >> 4, rem = t & 15, r = rem >> 1, c = rem & 1;
-      if (g.cy0 + r < F.ch) {
-        const float4* src = reinterpret_cast<const float4*>(L.csum[pl] + r * WCW + 8 * c);
-        const float4 v0 = src[0], v1 = src[1];
-        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        unsigned code[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
-        auto put = [&](auto plane) {
-          constexpr int P = decltype(plane)::value;
-          const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + P] + g.f * F.out_fp[1 + P], F.out_bytes[1 + P]);
-          const int so = g.cy0 * (int)F.out_ls[1 + P];
-          if (F.out8)
-            __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
-                                                   code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
-                oc_, lofs.sc, so + g.cx0, NT);
-          else
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
-                                                   code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
-                oc_, lofs.sc, so + 2 * g.cx0, NT);
-        };
-        if (pl == 0)
-          put(std::integral_constant<int, 0>());
-        else
-          put(std::integral_constant<int, 1>());
-      }
-    }
-    if (!more) break;
-    q = nq;
-    // the stores above have read yin / csum before the next commit refills them
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
-
 #define FAST_CASES(X) \
   X(0, 4, 0, 0)       \
   X(0, 4, 1, 0)       \
@@ -1089,10 +824,7 @@ hipError_t launch_tile(const FastParams& F, int trc, int tm, int desat, int lp, 
                        hipStream_t s) {
 #define X(T, M, D, L)                                                                     \
   if (trc == T && tm == M && desat == D && lp == L) {                                     \
-    if (F.kernel == 1)                                                                    \
-      hipLaunchKernelGGL((k_wave<T, M, D, L, DBG>), grid, dim3(256), lds, s, F);          \
-    else                                                                                  \
-      hipLaunchKernelGGL((k_tile<T, M, D, L, DBG>), grid, dim3(256), lds, s, F);          \
+    hipLaunchKernelGGL((k_tile<T, M, D, L, DBG>), grid, dim3(256), lds, s, F);            \
     return hipGetLastError();                                                             \
   }
   FAST_CASES(X)

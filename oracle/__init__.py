@@ -219,25 +219,50 @@ def pq_eotf_d(e: float) -> float:
     return (max(xp - c1, 0.0) / (c2 - c3 * xp)) ** (1 / m1)
 
 
-class PeakState:
-    """Restatement of the dynamic-peak smoothing (h2s_api.hip peak_update):
-    IIR with time constant 20 frames on the PQ max / average, bypassed by a
-    smoothstep over 10..30 % PQ average change; peak clamped to [1, static]."""
+def _nan_or(v, d):
+    return d if v is None or (isinstance(v, float) and math.isnan(v)) else v
 
-    def __init__(self):
+
+class PeakState:
+    """Restatement of the dynamic-peak smoothing (h2s_api.hip peak_update;
+    PARITY UNPINNED): IIR with coefficient 1 - exp(-1 / smoothing_period) on
+    the PQ peak measurement / average, bypassed by a smoothstep over the
+    scene-change band (% PQ average change); the peak clamped to
+    [minimum_peak x SDR white, static].  Defaults: vf_libplacebo's options
+    (100 frames, 5.5 / 10 %, minimum_peak 1.0) for ``params`` with NaN
+    fields; ``params`` None keeps those defaults with a 203-nit white."""
+
+    def __init__(self, params=None, **kw):
         self.frames, self.max, self.avg = 0, 0.0, 0.0
+
+        def g(n, d):
+            if n in kw:
+                return kw[n]
+            return _nan_or(getattr(params, n, None), d) if params is not None else d
+        self.smoothing = g('pd_smoothing', 100.0)
+        self.lo, self.hi = g('pd_scene_low', 5.5), g('pd_scene_high', 10.0)
+        white = 203.0
+        if params is not None:
+            lp = params.pipeline == 2 or (params.pipeline == 0 and params.tonemap in (7, 8))
+            white = _nan_or(params.target_white, 203.0 if lp else params.npl)
+        white = kw.get('white', white)
+        self.min_peak = g('pd_min_peak', 1.0) * white / 100.0
 
     def update(self, fmax: float, favg: float, static_peak: float) -> float:
         if self.frames == 0:
             self.max, self.avg = fmax, favg
         else:
-            a = 1.0 - math.exp(-1.0 / 20.0)
-            t = min(max((abs(favg - self.avg) * 100.0 - 10.0) / 20.0, 0.0), 1.0)
+            a = 1.0 - math.exp(-1.0 / self.smoothing) if self.smoothing > 0 else 1.0
+            d = abs(favg - self.avg) * 100.0
+            t = 0.0
+            if self.lo >= 0 and self.hi >= 0:
+                t = (d - self.lo) / (self.hi - self.lo) if self.hi > self.lo else (1.0 if d >= self.lo else 0.0)
+            t = min(max(t, 0.0), 1.0)
             w = a + (1.0 - a) * t * t * (3.0 - 2.0 * t)
             self.max += w * (fmax - self.max)
             self.avg += w * (favg - self.avg)
         self.frames += 1
-        return min(max(pq_eotf_d(self.max) * 100.0, 1.0), static_peak)
+        return min(max(pq_eotf_d(self.max) * 100.0, self.min_peak), static_peak)
 
 
 def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
@@ -245,7 +270,7 @@ def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarra
     """BT.2390 / spline with the detected peak: stats, smoothing, then each
     frame through the chain with its own peak (and, for spline, the smoothed
     average as the knee source).  Returns (frames, peaks)."""
-    state = state or PeakState()
+    state = state or PeakState(params)
     static_peak = resolved(params)[0]
     fmax, favg = peak_stats(params, buf, width, height)
     outs, peaks = [], []

@@ -90,6 +90,10 @@ typedef struct {
   double n_peak;        /* libplacebo NORM curves: source peak / target white */
   double r2l[3][3], l2r[3][3]; /* BT.2020 RGB -> LMS (HPE), inverse           */
   int dither;           /* 1: ordered dither at the swscale 8-bit quantiser */
+  /* libplacebo stage options (include/h2s.h ABI v3) */
+  float lp_qs, lp_qo;   /* rgba8 code = floor(v lp_qs + lp_qo + offset): range=tv model */
+  int lp_dith;          /* offset = 16 x 16 Bayer (h2s_lp_dither ORDERED), else 0.5     */
+  int in_mask;          /* input code mask: 0xFFFC = 12-bit input, p010 TRUNCATE         */
 } ocfg;
 
 /* ---- S1 helpers -------------------------------------------------------- */
@@ -498,11 +502,24 @@ static float lp_encode(const ocfg *c, float x) {
   return powf(x / (float)c->enc_a, 1.0f / 2.4f) - (float)c->enc_b;
 }
 
-/* libplacebo branch: the 8-bit rgba download (round to nearest, no dither:
- * libplacebo's default blue-noise dither is not restated) */
-static int rgba8_q(float v) {
+/* 16 x 16 Bayer matrix (M_2n = 4 M_n + M_1 per 2 x 2 block, M_1 = [0 2; 3 1])
+ * as an offset (M + 0.5) / 256: the h2s_lp_dither ORDERED model (a stand-in
+ * for libplacebo's default blue-noise dither, which is not restated) */
+static float bayer16(int x, int y) {
+  int m = 0;
+  for (int i = 0; i < 4; i++) {
+    int bx = (x >> i) & 1, by = (y >> i) & 1;
+    m += (2 * (bx ^ by) + by) << (2 * (3 - i));
+  }
+  return ((float)m + 0.5f) * (1.0f / 256.0f);
+}
+
+/* libplacebo branch: the 8-bit rgba download of pixel (x, y): round to
+ * nearest (h2s_lp_dither NONE) or the ordered offset, full-range codes or
+ * range=tv's limited-range RGB (h2s_lp_range LIMITED: 16 + 219 v) */
+static int rgba8_q(const ocfg *c, float v, int x, int y) {
   v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-  return (int)floorf(v * 255.0f + 0.5f);
+  return (int)floorf(v * c->lp_qs + (c->lp_qo + (c->lp_dith ? bayer16(x, y) : 0.5f)));
 }
 
 /* vf_lut3d's 8-bit packed path (interp_8_tetrahedral): coordinate
@@ -546,8 +563,8 @@ static rgbf lut3d_16bit(const ocfg *c, int r16, int g16, int b16) {
  * libplacebo branch: stage 3 = BT.1886 (target black) R'G'B' before the
  * download, stage 4 = lut3d's 8-bit output / 255 (LUT on) or the encoded
  * BT.709 R'G'B' (LUT off: libplacebo's own gamut conversion, clipped). */
-static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf *dbg) {
-  (void)dbg;
+static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, int px, int py) {
+  (void)px, (void)py;
   rgbf e;
   e.r = y + c->m_rcr * cr;
   e.g = y + c->m_gcb * cb + c->m_gcr * cr;
@@ -577,7 +594,7 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, rgbf 
       g.g = lp_encode(c, t.g);
       g.b = lp_encode(c, t.b);
       if (upto == H2S_STAGE_GAMMA) return g;
-      rgbf q = lut3d_8bit(c, rgba8_q(g.r), rgba8_q(g.g), rgba8_q(g.b));
+      rgbf q = lut3d_8bit(c, rgba8_q(c, g.r, px, py), rgba8_q(c, g.g, px, py), rgba8_q(c, g.b, px, py));
       rgbf o = {q.r / 255.0f, q.g / 255.0f, q.b / 255.0f};
       return o;
     }
@@ -665,6 +682,13 @@ static int resolve(ocfg *c, const h2s_params *p, const float *lut, int n) {
   else
     c->q_bits = 8;
   c->dither = p->dither == H2S_DITHER_ORDERED && c->q_bits == 8;
+  {
+    const int lp = c->pipe == H2S_PIPE_LIBPLACEBO, lim = lp && p->lp_range == H2S_LP_RANGE_LIMITED;
+    c->lp_qs = lim ? 219.0f : 255.0f;
+    c->lp_qo = lim ? 16.0f : 0.0f;
+    c->lp_dith = lp && p->lp_dither == H2S_LP_DITHER_ORDERED;
+    c->in_mask = lp && p->lp_p010 == H2S_LP_P010_TRUNCATE && p->bits_in == 12 ? 0xFFFC : 0xFFFF;
+  }
 
   /* vf_tonemap init: parameter defaults */
   double param = p->tm_param;
@@ -802,7 +826,7 @@ static inline int edge_m(int i, int n, int mode) {
 /* normalised chroma sample */
 static inline float csamp(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
   const int m = c->p->chroma_edge;
-  return (float)rd(in, plane, frame, edge_m(x, cw, m), edge_m(y, ch, m)) * c->c_scale + c->c_off;
+  return (float)(rd(in, plane, frame, edge_m(x, cw, m), edge_m(y, ch, m)) & c->in_mask) * c->c_scale + c->c_off;
 }
 
 /* horizontal pass (left siting): luma column x from chroma row cy */
@@ -859,10 +883,10 @@ static yuvf px_yuv(const ocfg *c, const h2s_frames *in, int f, int x, int y) {
   float s = (float)(1 << (c->q_bits - 8));
   const float cbr = (float)(-0.2126 / 1.8556), cbg = (float)(-0.7152 / 1.8556), cbb = (float)(0.9278 / 1.8556);
   const float crr = (float)(0.7874 / 1.5748), crg = (float)(-0.7152 / 1.5748), crb = (float)(-0.0722 / 1.5748);
-  float yv = (float)rd(in, 0, f, x, y) * c->y_scale + c->y_off;
+  float yv = (float)(rd(in, 0, f, x, y) & c->in_mask) * c->y_scale + c->y_off;
   float cb = upsample(c, in, 1, f, x, y, cw, ch);
   float cr = upsample(c, in, 2, f, x, y, cw, ch);
-  rgbf o = chain_px(c, yv, cb, cr, 99, NULL);
+  rgbf o = chain_px(c, yv, cb, cr, 99, x, y);
   float R = clipf(o.r, 0.0f, 1.0f), G = clipf(o.g, 0.0f, 1.0f), B = clipf(o.b, 0.0f, 1.0f);
   float Y = K709_R * R + K709_G * G + K709_B * B;
   yuvf r = {(16.0f + 219.0f * Y) * s, cbr * R + cbg * G + cbb * B, crr * R + crg * G + crb * B};
@@ -1031,10 +1055,10 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
         out_rgb[2 * plane + i] = 224.0f * s * v.cr;
         continue;
       }
-      float yv = (float)rd(in, 0, 0, x, y) * c.y_scale + c.y_off;
+      float yv = (float)(rd(in, 0, 0, x, y) & c.in_mask) * c.y_scale + c.y_off;
       float cb = upsample(&c, in, 1, 0, x, y, cw, ch);
       float cr = upsample(&c, in, 2, 0, x, y, cw, ch);
-      rgbf o = chain_px(&c, yv, cb, cr, stage, NULL);
+      rgbf o = chain_px(&c, yv, cb, cr, stage, x, y);
       out_rgb[i] = o.r;
       out_rgb[plane + i] = o.g;
       out_rgb[2 * plane + i] = o.b;
@@ -1148,10 +1172,35 @@ int oracle_preview_tail(const uint8_t *yuv8, int W, int H, int ow, int oh, doubl
 }
 
 /* ---- dynamic peak statistics (params.peak_detect, BT.2390) ---------------
- * PARITY UNPINNED (libplacebo absent): per frame, max and mean of the
- * PQ-encoded max(R,G,B) over every pixel, nearest chroma; the smoothing is
- * restated in oracle/__init__.py (PeakState). */
+ * PARITY UNPINNED (libplacebo absent): per frame, the peak measurement and
+ * the mean of the PQ-encoded max(R,G,B) over every pixel, nearest chroma.
+ * The peak measurement is the maximum (pd_percentile 100) or the
+ * pd_percentile-th percentile (NaN: vf_libplacebo's 99.995) from a 1024-bin
+ * histogram over PQ [0, 1], interpolated linearly inside the bin that
+ * reaches it and capped at the maximum.  The smoothing is restated in
+ * oracle/__init__.py (PeakState). */
+#define PEAK_BINS 1024
+static double pq_percentile(const unsigned *h, int nb, double pct, double mx) {
+  double n = 0.0, cum = 0.0;
+  for (int i = 0; i < nb; i++) n += h[i];
+  const double target = pct / 100.0 * n;
+  for (int i = 0; i < nb; i++) {
+    if (h[i] && cum + h[i] >= target) {
+      const double v = (i + (target - cum) / h[i]) / nb;
+      return v < mx ? v : mx;
+    }
+    cum += h[i];
+  }
+  return mx;
+}
+
 int oracle_peak_stats(const h2s_params *p, const h2s_frames *in, int nframes, double *fmax, double *favg) {
+  const double pct = isnan(p->pd_percentile) ? 99.995 : p->pd_percentile;
+  const int lp = p->pipeline == H2S_PIPE_LIBPLACEBO ||
+                 (p->pipeline == H2S_PIPE_AUTO && (p->tonemap == H2S_TM_BT2390 || p->tonemap == H2S_TM_SPLINE));
+  const int mask = lp && p->lp_p010 == H2S_LP_P010_TRUNCATE && p->bits_in == 12 ? 0xFFFC : 0xFFFF;
+  unsigned *hist = (unsigned *)malloc(PEAK_BINS * sizeof(unsigned));
+  if (!hist) return H2S_E_OOM;
   const int sh = p->bits_in - 8;
   const double ys = 1.0 / (219 << sh), yo = -(double)(16 << sh) / (219 << sh);
   const double cs = 1.0 / (224 << sh), co = -(double)(128 << sh) / (224 << sh);
@@ -1160,10 +1209,11 @@ int oracle_peak_stats(const h2s_params *p, const h2s_frames *in, int nframes, do
   const int W = in->width, H = in->height;
   for (int f = 0; f < nframes; f++) {
     double mx = 0, sm = 0;
+    memset(hist, 0, PEAK_BINS * sizeof(unsigned));
     for (int y = 0; y < H; y++)
       for (int x = 0; x < W; x++) {
-        const double Y = rd(in, 0, f, x, y) * ys + yo;
-        const double cb = rd(in, 1, f, x / 2, y / 2) * cs + co, cr = rd(in, 2, f, x / 2, y / 2) * cs + co;
+        const double Y = (rd(in, 0, f, x, y) & mask) * ys + yo;
+        const double cb = (rd(in, 1, f, x / 2, y / 2) & mask) * cs + co, cr = (rd(in, 2, f, x / 2, y / 2) & mask) * cs + co;
         const double er = Y + mrcr * cr, eg = Y + mgcb * cb + mgcr * cr, eb = Y + mbcb * cb;
         double m;
         if (p->transfer_in == H2S_TRC_HLG) {
@@ -1181,9 +1231,12 @@ int oracle_peak_stats(const h2s_params *p, const h2s_frames *in, int nframes, do
         m = m < 0 ? 0 : (m > 1 ? 1 : m);
         mx = m > mx ? m : mx;
         sm += m;
+        const int b = (int)(m * PEAK_BINS);
+        hist[b < PEAK_BINS - 1 ? b : PEAK_BINS - 1]++;
       }
-    fmax[f] = mx;
+    fmax[f] = pct < 100.0 ? pq_percentile(hist, PEAK_BINS, pct, mx) : mx;
     favg[f] = sm / ((double)W * H);
   }
+  free(hist);
   return 0;
 }

@@ -141,3 +141,43 @@ def test_libplacebo_chain_with_other_operators_is_rejected(tm):
     chain = f'libplacebo=w=iw:h=ih:tonemapping={tm}:peak_detect=1:format=rgba,hwdownload,format=rgba'
     with pytest.raises(ValueError):
         parse_filter_chain(chain)
+
+
+# ---- the libplacebo stage: only the option values the engine models ---------
+_LP = ('format=p010,hwupload,libplacebo=w=iw:h=ih:tonemapping=bt.2390:colorspace=bt709:'
+       'color_primaries={prim}:color_trc=bt709:range={rng}:peak_detect=1:format={fmt}{extra},'
+       'hwdownload,format={fmt}{lut}')
+_LUT = ',lut3d=file=<LUT>:interp=tetrahedral,setparams=color_primaries=bt709:color_trc=bt709:colorspace=bt709'
+
+
+def _lp(prim='auto', rng='tv', fmt='rgba', extra='', lut=_LUT):
+    return _LP.format(prim=prim, rng=rng, fmt=fmt, extra=extra, lut=lut)
+
+
+def test_libplacebo_reference_options_parse():
+    """Both forms build_libplacebo_filter emits (src/utils.py:445-449): LUT
+    on (primaries auto, rgba) and off (bt709, nv12)."""
+    p, lut = hdr2sdr.parse_filter_chain(_lp())
+    assert p.pipeline == 'libplacebo' and p.lut_enabled and lut == '<LUT>' and p.peak_detect
+    assert p.lp_range == 'full'
+    p, lut = hdr2sdr.parse_filter_chain(_lp(prim='bt709', fmt='nv12', lut=''))
+    assert not p.lut_enabled and lut is None
+    p, _ = hdr2sdr.parse_filter_chain(_lp(rng='pc'))      # full range: no model choice left
+    assert p.lp_range == 'full'
+    p, _ = hdr2sdr.parse_filter_chain(_lp(), lp_range='limited')   # range=tv follows the model switch
+    assert p.lp_range == 'limited'
+
+
+@pytest.mark.parametrize('chain', [
+    _lp(rng='jpeg'),                                   # range value not modelled
+    _lp(extra=':dithering=blue'),                      # option not modelled
+    _lp(extra=':percentile=99.9'),                     # peak-detect options are h2s_params fields, not parsed
+    _lp().replace('color_trc=bt709', 'color_trc=smpte2084'),
+    _lp().replace('colorspace=bt709', 'colorspace=bt2020nc'),
+    _lp().replace('w=iw', 'w=1920'),                   # scaling (the preview's job)
+    _lp(prim='bt709'),                                 # libplacebo gamut mapping and the LUT: a double conversion
+    _lp(prim='auto', fmt='nv12', lut=''),              # no gamut conversion at all
+])
+def test_libplacebo_unmodelled_options_are_rejected(chain):
+    with pytest.raises(ValueError):
+        hdr2sdr.parse_filter_chain(chain)

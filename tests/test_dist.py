@@ -120,13 +120,13 @@ class _OracleTM:
         import oracle
         self.o, self.p, self.lat = oracle, oracle.params_from(params.to_c()), lattice
         self.static = oracle.resolved(self.p)[0]
-        self.state = oracle.PeakState()
+        self.state = oracle.PeakState(self.p)
 
     def peak_stats(self, shard):
         return self.o.peak_stats(self.p, shard.buf, PW, PH)
 
     def reset_peak(self):
-        self.state = self.o.PeakState()
+        self.state = self.o.PeakState(self.p)
 
     def feed_peak(self, fmax, favg):
         for m, a in zip(fmax, favg):
@@ -144,7 +144,7 @@ def _peak_worker(rank, world, port, out_dir, sync):
 
     from hdr2sdr import FrameBatch, TonemapParams, generate_lattice
     from hdr2sdr.dist import frame_checksum, reduce_run, shard_range, sync_peak_state
-    from test_peak_detect import sequence
+    from test_peak_detect import ROUND2, sequence
 
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -152,7 +152,8 @@ def _peak_worker(rank, world, port, out_dir, sync):
         buf = sequence(PW, PH)
         n = buf.shape[0]
         a, b = shard_range(n, world, rank)
-        tm = _OracleTM(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0), generate_lattice(17))
+        tm = _OracleTM(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0, **ROUND2),
+                       generate_lattice(17))
         shard = FrameBatch(np.ascontiguousarray(buf[a:b]), PW, PH, 10)
         if sync:
             sync_peak_state(tm, shard, n)
@@ -171,10 +172,10 @@ def test_gloo_world2_dynamic_peak_equals_sequential(tmp_path):
     import oracle
     from hdr2sdr import TonemapParams, generate_lattice
     from hdr2sdr.dist import frame_checksum
-    from test_peak_detect import sequence
+    from test_peak_detect import ROUND2, sequence
 
     buf = sequence(PW, PH)
-    p = oracle.params_from(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0).to_c())
+    p = oracle.params_from(TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0, **ROUND2).to_c())
     seq_out, seq_peaks = oracle.process_dynamic(p, generate_lattice(17), buf, PW, PH)
     want = frame_checksum(seq_out, 0)
     world = 2

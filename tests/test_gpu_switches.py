@@ -113,6 +113,14 @@ LP_CASES = {
     'lp_reinhard_hlg12_lut_off': dict(tonemapper='reinhard', pipeline='libplacebo', bits_in=12, bits_out=12,
                                       transfer='arib-std-b67', lut_enabled=False),
     'lp_mobius_gamma13': dict(tonemapper='mobius', pipeline='libplacebo', gamma=1.3),
+    # the stage's open options (ABI v3; include/h2s.h enum h2s_lp_range / _dither / _p010)
+    'bt2390_range_limited': dict(tonemapper='bt.2390', lp_range='limited'),
+    'bt2390_dither_ordered': dict(tonemapper='bt.2390', lp_dither='ordered'),
+    'spline_limited_dither_8bit': dict(tonemapper='spline', lp_range='limited', lp_dither='ordered', bits_out=8),
+    'bt2390_pq12_p010_keep': dict(tonemapper='bt.2390', bits_in=12, bits_out=10),
+    'bt2390_pq12_p010_truncate': dict(tonemapper='bt.2390', bits_in=12, bits_out=10, lp_p010='truncate'),
+    'lp_hable_hlg12_p010_truncate_dither': dict(tonemapper='hable', pipeline='libplacebo', bits_in=12, bits_out=12,
+                                               transfer='arib-std-b67', lp_p010='truncate', lp_dither='ordered'),
 }
 
 
@@ -130,7 +138,8 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
 
 @pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb',
                                   'bt2390_lut_off_nv12', 'bt2390_max_rgb_lut_off', 'lp_hable', 'lp_mobius_max_rgb',
-                                  'lp_reinhard_hlg12_lut_off'])
+                                  'lp_reinhard_hlg12_lut_off', 'bt2390_range_limited', 'bt2390_dither_ordered',
+                                  'bt2390_pq12_p010_truncate', 'lp_hable_hlg12_p010_truncate_dither'])
 def test_libplacebo_tile_equals_generic(tm, case):
     """The two kernels of the libplacebo branch against each other (same
     device, same float32 formulas up to the tile kernel's PQ table): the
@@ -147,6 +156,32 @@ def test_libplacebo_tile_equals_generic(tm, case):
         tm.set_option(_abi.OPT_FAST_PATH, 1)
     assert_close_int(params, tile, gen, 256, 64)
     assert (tile == gen).mean() > 0.99
+
+
+@pytest.mark.parametrize('kw,min_changed', [
+    (dict(lp_range='limited'), 0.5),                          # every code moves towards mid-grey
+    (dict(lp_dither='ordered'), 0.02),                        # a fraction of the codes step by one
+    (dict(lp_p010='truncate', bits_in=12), 0.02),             # 12-bit input: two low bits dropped
+])
+def test_libplacebo_options_change_the_output(tm, kw, min_changed):
+    base = hdr2sdr.TonemapParams(tonemapper='bt.2390', bits_in=kw.get('bits_in', 10))
+    src = synth_frames('smooth', 1, 256, 64, base.bits_in, device='cpu', seed=8).to_torch('cuda')
+    tm.set_params(base)
+    tm.set_lut(lattice(65))
+    a = tm(src).to_numpy().buf
+    tm.set_params(base.with_(**kw))
+    b = tm(src).to_numpy().buf
+    assert (a != b).mean() > min_changed
+
+
+def test_p010_truncate_has_no_effect_on_10bit_input(tm):
+    p = hdr2sdr.TonemapParams(tonemapper='bt.2390')
+    src = synth_frames('uniform', 1, 128, 64, 10, device='cpu', seed=9).to_torch('cuda')
+    tm.set_params(p)
+    tm.set_lut(lattice(65))
+    a = tm(src).to_numpy().buf
+    tm.set_params(p.with_(lp_p010='truncate'))
+    assert np.array_equal(tm(src).to_numpy().buf, a)
 
 
 def test_lp_tone_ipt_changes_only_coloured_pixels(tm):

@@ -1,12 +1,17 @@
 """Dynamic peak for BT.2390 (libplacebo peak_detect=1, src/utils.py:448).
 
 PARITY UNPINNED against libplacebo (not in this image).  The model is stated
-in DESIGN.md and restated in the oracle: per-frame max / mean of the
-PQ-encoded max(R,G,B), an IIR with a 20-frame time constant that a
-smoothstep over a 10..30 % PQ change of the average bypasses at scene cuts,
-and the result clamped to [1, static peak].  The GPU path (per-frame stats
-kernel + host smoothing + per-frame BT.2390 constants) must match that
-restatement frame by frame, across calls on one context."""
+in DESIGN.md §4.6 and restated in the oracle: per frame a peak measurement
+(the pd_percentile-th percentile of the PQ-encoded max(R,G,B), from a
+1024-bin histogram; the maximum at 100) and the mean; an IIR with
+coefficient 1 - exp(-1 / pd_smoothing) that a smoothstep over a
+pd_scene_low .. pd_scene_high % PQ change of the average bypasses at scene
+cuts; the result clamped to [pd_min_peak x SDR white, static peak].
+Defaults: vf_libplacebo's options (100 frames, 5.5 / 10 %, 99.995, 1.0);
+ROUND2 below is round 2's fixed model (20 frames, 10 / 30 %, maximum, 100
+nits).  The GPU path (per-frame stats kernel + host smoothing + per-frame
+curve constants) must match that restatement frame by frame, across calls
+on one context."""
 import math
 
 import numpy as np
@@ -17,8 +22,12 @@ import hdr2sdr
 from hdr2sdr.synth import synth_frames
 
 
+# round 2's fixed model; its 100-nit floor as a fraction of the 203-nit SDR white
+ROUND2 = dict(pd_smoothing=20.0, pd_scene_low=10.0, pd_scene_high=30.0, pd_percentile=100.0, pd_min_peak=100.0 / 203.0)
+
+
 def test_peak_state_first_frame_constant_and_scene_cut():
-    st = oracle.PeakState()
+    st = oracle.PeakState(**{k: v for k, v in ROUND2.items() if k != 'pd_percentile'})
     p0 = st.update(0.6, 0.3, 40.0)
     assert p0 == pytest.approx(oracle.pq_eotf_d(0.6) * 100)
     for _ in range(5):                               # constant input: constant peak
@@ -29,11 +38,38 @@ def test_peak_state_first_frame_constant_and_scene_cut():
     assert st.max == pytest.approx(0.9) and st.avg == pytest.approx(0.8)
 
 
-def test_peak_clamps_to_one_and_static_peak():
+def test_peak_state_vf_libplacebo_defaults():
+    """smoothing_period 100, scene thresholds 5.5 / 10 % PQ of the average"""
     st = oracle.PeakState()
-    assert st.update(0.1, 0.05, 10.0) == 1.0         # below 100 nits -> 1
+    st.update(0.6, 0.3, 40.0)
+    st.update(0.7, 0.33, 40.0)                       # 3 % change: plain IIR step, 1 - exp(-1/100)
+    assert st.max == pytest.approx(0.6 + (1 - math.exp(-1 / 100)) * 0.1)
+    st.update(0.9, 0.6, 40.0)                        # 27 % > 10 %: full bypass
+    assert st.max == pytest.approx(0.9) and st.avg == pytest.approx(0.6)
+    a = 1 - math.exp(-1 / 100)
+    st.update(0.5, 0.6 + 0.0775, 40.0)               # 7.75 %: half-way through the band, smoothstep 0.5
+    assert st.max == pytest.approx(0.9 + (a + (1 - a) * 0.5) * (0.5 - 0.9))
+
+
+def test_peak_clamps_to_minimum_and_static_peak():
     st = oracle.PeakState()
-    assert st.update(0.95, 0.5, 10.0) == 10.0        # above the static peak -> static
+    assert st.update(0.1, 0.05, 10.0) == pytest.approx(2.03)   # minimum_peak 1.0 x the 203-nit SDR white
+    st = oracle.PeakState(**ROUND2)
+    assert st.update(0.1, 0.05, 10.0) == pytest.approx(1.0)    # round 2: 100 nits
+    st = oracle.PeakState()
+    assert st.update(0.95, 0.5, 10.0) == 10.0                  # above the static peak -> static
+
+
+def test_oracle_percentile_cuts_isolated_highlights():
+    """99.995 % of 256 x 256 pixels cuts the brightest 3.3 pixels' worth, so
+    two isolated super-bright pixels do not set the peak; 100 = the maximum."""
+    fb = _flat_frame(64 + round(0.5 * 876), W=256, H=256)
+    fb.y[0, 0, :2] = 940                             # two pixels at E = 1
+    p = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True)
+    mx, _ = oracle.peak_stats(oracle.params_from(p.to_c()), fb.buf, 256, 256)
+    assert mx[0] < 0.51
+    mx, _ = oracle.peak_stats(oracle.params_from(p.with_(pd_percentile=100.0).to_c()), fb.buf, 256, 256)
+    assert mx[0] == pytest.approx(1.0)
 
 
 def _flat_frame(code_y, code_c=512, W=64, H=32):
@@ -71,13 +107,15 @@ def sequence(W=256, H=128):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('model', ['vf_libplacebo', 'round2'])
 @pytest.mark.parametrize('pipeline', ['cpu', 'libplacebo'])  # cpu: the tile kernel's per-frame curve records
 @pytest.mark.parametrize('tmname', ['bt.2390', 'spline'])   # spline also takes its knee from the average
 @pytest.mark.parametrize('W,H', [(256, 128), (192, 96), (200, 96)])   # fast path (blocks within / across frames), + tail
-def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline):
+def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline, model):
     from test_gpu_parity import assert_close_int, lattice
     buf = sequence(W, H)
-    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0, pipeline=pipeline)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0, pipeline=pipeline,
+                                   **(ROUND2 if model == 'round2' else {}))
     tm = hdr2sdr.Tonemapper(0, params, lattice(65))
     got = []
     for a, b in ((0, 2), (2, 5), (5, 6)):            # the state carries across calls

@@ -148,6 +148,26 @@ def test_no_cpu_chain_curve_matches_it(model):
         assert min(mae_oracle(model, tonemapper=tm, peak=p) for p in PEAKS) > best + 1.0
 
 
+@pytest.mark.parametrize('model', sorted(MODELS))
+def test_libplacebo_range_tv_keeps_full_range_rgba(model):
+    """h2s_lp_range: range=tv on the rgba download read as limited-range RGB
+    (16..235, then treated as full range by lut3d and the auto-scale) is the
+    rival explanation of the lifted blacks; it fits 4x worse (13.2 / 12.5
+    against 3.17 / 2.09 per 255), with or without the black-point lift, so
+    the full-range default stands."""
+    best = best_fit(model)
+    assert best_fit(model, (('lp_range', 'limited'),)) > best + 5.0
+    assert best_fit(model, (('lp_range', 'limited'), ('target_black', 0.0))) > best + 5.0
+
+
+@pytest.mark.parametrize('model', sorted(MODELS))
+def test_libplacebo_download_dither_not_separated(model):
+    """h2s_lp_dither: the ordered stand-in for libplacebo's dither moves the
+    fit by < 0.05 per 255 (3.144 / 2.099 against 3.174 / 2.094): the pair
+    cannot tell dithered from rounded downloads; the default stays none."""
+    assert abs(best_fit(model, (('lp_dither', 'ordered'),)) - best_fit(model)) < 0.1
+
+
 def c3_params():
     """The reference's own C3 chain (captured argv) parsed, at 8-bit output."""
     import json
@@ -169,6 +189,10 @@ def test_reference_c3_settings_without_fitting(model):
     assert p.peak_detect and p.resolved_pipeline() == 'libplacebo' and p.tonemapper == 'bt.2390'
     ipt, peak = mae_dynamic(model, p)
     assert peak == pytest.approx(10.0)        # detected 1796 nits, capped at the 1000-nit default
+    # one frame: the smoothing / scene thresholds do not act, and the
+    # 99.995th percentile (vf_libplacebo's default) is above the cap as well
+    for kw in (dict(pd_percentile=100.0), dict(pd_smoothing=20.0, pd_scene_low=10.0, pd_scene_high=30.0)):
+        assert mae_dynamic(model, p.with_(**kw)) == (ipt, peak)
     assert ipt < BEST_BOUND[model]
     assert mae_dynamic(model, p.with_(lp_tone='max-rgb'))[0] > ipt + 0.3
 
