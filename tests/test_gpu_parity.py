@@ -259,11 +259,14 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     q = oracle.quant_bits(op)
     # The 6e-4 floor on stages 3/4 belongs to k_tile's PQ EOTF table (its first
     # segment); the generic kernel evaluates the EOTF with powf and keeps the
-    # round-1 floor of 1e-5 on every stage.
+    # round-1 floor of 1e-5, except at stage 4, where the lattice's gamut-clip
+    # bend next to black multiplies the PQ pow's float32 disagreement
+    # (~4e-5 relative at stage 1, any two implementations) by its slope:
+    # measured 5.0e-5 absolute at most ('uniform', R'G'B' ~0.011), floor 1e-4.
     if kernel == 'k_tile':
         floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
     else:
-        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-5, 5: 1e-5}[stage]
+        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-4, 5: 1e-5}[stage]
     got = got.astype(np.float64)
     with np.errstate(invalid='ignore'):
         err = np.abs(got - want)
