@@ -52,6 +52,8 @@ def parse_args():
     ap.add_argument('--mode', default='compat8')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline budget (0 = skip)')
     ap.add_argument('--no-alt', action='store_true', help='skip the uniform-content secondary run')
+    ap.add_argument('--no-sharded', action='store_true',
+                    help='skip the sharded C4 / C5 lines (profiling runs of the headline kernel alone)')
     ap.add_argument('--dry-run', action='store_true',
                     help='launch + collectives only, no GPU work (CPU test of the multi-rank flow)')
     return ap.parse_args()
@@ -374,7 +376,7 @@ def main():
     # rank exactly as the headline (barrier + synchronize around the timed
     # launches, MAX of the elapsed time over ranks, SUM of pixels)
     sharded = {}
-    for tag, workload, kw, w_, h_, fpr, lut_n in SHARDED:
+    for tag, workload, kw, w_, h_, fpr, lut_n in (() if args.no_sharded else SHARDED):
         p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
         lat_ = hdr2sdr.generate_lattice(lut_n) if rank == 0 else None
         if world > 1:

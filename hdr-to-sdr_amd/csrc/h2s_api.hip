@@ -18,7 +18,8 @@ hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
 hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s);
 bool fast_supported(int tonemap);
 hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg = 0);
-hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
+hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s);
+hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
                             long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
@@ -963,6 +964,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->eq_n = k.qmax + 1;
   F->c_bias = 128.0f * k.qscale + 0.5f;
   F->shift_out = k.shift_out;
+  F->rep_rs = k.expand_rep && k.shift_out ? 8 - k.shift_out : 31;
+  F->dither = k.dither;
   F->out8 = p->bits_out == 8 ? 1 : 0;
   F->pq_tab = c->d_pq;
 }
@@ -1046,7 +1049,42 @@ static hipError_t launch_two_pass_frames(const h2s_ctx* c, const KParams& k, boo
     kf.nframes = 1;
     kf.total = (long long)kf.ch * kf.ngx;
     kf.chr444 = c->d_chr;
-    hipError_t e = h2s::launch_two_pass(kf, wx, wy, out8, s);
+    hipError_t e = h2s::launch_process_c444(kf, out8, s);
+    if (e == hipSuccess) e = h2s::launch_chroma_bicubic(kf, wx, wy, out8, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
+                               hipStream_t s, const h2s::CurveConsts* cvf, bool tail, int dbg, float* dbg_out,
+                               float2* chr444);
+
+// BICUBIC chroma with the tile kernel, frame by frame: k_tile writes luma
+// and every pixel's (Cb, Cr) into the context scratch (the generic C444
+// kernel covers the width % 64 columns), then the decimation pass
+static hipError_t launch_tile_two_pass(const h2s_ctx* c, const KParams& k, bool out8, int nframes, hipStream_t s) {
+  float wx[7], wy[8];
+  chroma_taps(wx, wy);
+  for (int f = 0; f < nframes; f++) {
+    KParams kf = k;
+    for (int p = 0; p < 3; p++) {
+      kf.in[p] += f * kf.in_fp[p];
+      kf.out[p] += f * kf.out_fp[p];
+    }
+    kf.nframes = 1;
+    kf.total = (long long)kf.ch * kf.ngx;
+    kf.chr444 = c->d_chr;
+    hipError_t e = launch_chain(c, kf, true, false, out8, 1, s, nullptr, false, 0, nullptr, c->d_chr);
+    const int w64 = k.W & ~(h2s::TBW - 1);
+    if (e == hipSuccess && w64 != k.W) {
+      KParams kt = kf;
+      kt.gx0 = w64 / 8;
+      kt.ngx = (k.cw - w64 / 2 + 3) / 4;
+      kt.total = (long long)k.ch * kt.ngx;
+      e = h2s::launch_process_c444(kt, out8, s);
+    }
+    if (e == hipSuccess) e = h2s::launch_chroma_bicubic(kf, wx, wy, out8, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1058,11 +1096,12 @@ static hipError_t launch_two_pass_frames(const h2s_ctx* c, const KParams& k, boo
 // that stage, writing frame 0's planes to dbg_out
 static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
                                hipStream_t s, const h2s::CurveConsts* cvf = nullptr, bool tail = true, int dbg = 0,
-                               float* dbg_out = nullptr) {
+                               float* dbg_out = nullptr, float2* chr444 = nullptr) {
   if (!fast) {
     if (c->params.chroma_filter == H2S_CHROMA_BICUBIC) return launch_two_pass_frames(c, k, out8, nframes, s);
     return h2s::launch_process(k, vec, out8, s);
   }
+  if (c->params.chroma_filter == H2S_CHROMA_BICUBIC && !dbg && !chr444) return launch_tile_two_pass(c, k, out8, nframes, s);
   FastParams F;
   resolve_fast(c, k, &F);
   for (int p = 0; p < 3; p++) {
@@ -1089,6 +1128,9 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.dbg_w = k.W;
   F.dbg_lut = c->d_lut;
   F.inv_nm1 = 1.0f / (float)(c->lut_n - 1);
+  F.chr444 = chr444;
+  F.chr_w = k.W;
+  F.inv_c56 = 1.0f / F.c56;
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
   hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.pipe == h2s::PIPE_LIBPLACEBO ? 1 : 0, s, dbg);
   if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
@@ -1108,7 +1150,9 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   // CPU chain's legacy closed form stays on the generic kernel)
   if (!k.lut_enabled && k.pipe != h2s::PIPE_LIBPLACEBO) return false;
   if (k.lut_enabled && c->lut_n > 177) return false;
-  if (p.chroma_filter != H2S_CHROMA_BOX || k.dither || (k.expand_rep && k.shift_out) || k.lut_in16) return false;
+  if (k.lut_in16) return false;
+  // BICUBIC: the tile kernel runs pass 1 frame by frame (not under dynamic peak detection)
+  if (p.chroma_filter == H2S_CHROMA_BICUBIC && p.peak_detect) return false;
   return true;
 }
 
@@ -1468,7 +1512,9 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   const int path = choose_path(c, k, &din, &dout, out8);
   const bool fast = path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL;
   if (fast && k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) return rc;
-  if (path == H2S_PATH_TWO_PASS) {
+  // BICUBIC chroma (generic two-pass, or k_tile pass 1) uses the context scratch
+  const bool two_pass = c->params.chroma_filter == H2S_CHROMA_BICUBIC;
+  if (two_pass) {
     if ((rc = ensure_chr(c, k))) return rc;
     // one context scratch (d_chr) for every two-pass launch: a launch on
     // another stream waits until the previous one has finished with it
@@ -1518,7 +1564,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     e = copy_frames(out, &dout, nframes, s);
     if (e != hipSuccess) return hip_fail(c, e, "device->host copy");
   }
-  if (path == H2S_PATH_TWO_PASS) {
+  if (two_pass) {
     if ((e = hipEventRecord(c->chr_ev, s)) != hipSuccess) return hip_fail(c, e, "two-pass event");
     c->chr_pending = true;
   }

@@ -176,6 +176,13 @@ struct FastParams : CurveConsts {
   int eq_n;
   float c_bias;
   int shift_out, out8;
+  int rep_rs;                      // S8: 8 - shift_out (bit replication) or 31 (shift)
+  int dither;                      // S6 ordered dither at the 8-bit quantiser
+  // BICUBIC chroma (two-pass, one frame per launch): per-pixel (Cb, Cr) into
+  // chr444 (row pitch chr_w) instead of the 2x2 sums; inv_c56 = 1 / (56 q)
+  float2* chr444;
+  int chr_w;
+  float inv_c56;
   // S1 PQ EOTF (x 10000/npl) as a piecewise cubic: segment i covers
   // E in [i, i+1)/PQ_SEG, coefficients (c3, c2, c1, c0) of t = E*PQ_SEG - i
   const float4* pq_tab;

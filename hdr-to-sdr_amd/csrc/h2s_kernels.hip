@@ -308,14 +308,19 @@ hipError_t launch_debug(const KParams& P, int stage, float* out, hipStream_t s) 
   return hipGetLastError();
 }
 
-// BICUBIC chroma, one frame (P: nframes 1, in/out at that frame, chr444 set):
-// pass 1 = k_process<C444> (luma + per-pixel chroma), pass 2 = decimation
-hipError_t launch_two_pass(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s) {
+// BICUBIC chroma, pass 1 on the generic kernel: k_process<C444> (luma +
+// per-pixel chroma) over the launch's column groups (P.gx0, P.ngx)
+hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s) {
   constexpr int QPT = 4;
   const long long nb = (P.total + 255) / 256;
   if (nb == 0) return hipSuccess;
   if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
   else hipLaunchKernelGGL((k_process<QPT, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  return hipGetLastError();
+}
+
+// BICUBIC chroma, pass 2: the decimation of one frame's chr444
+hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s) {
   ChromaTaps T;
   for (int i = 0; i < 7; i++) T.wx[i] = wx7[i];
   for (int j = 0; j < 8; j++) T.wy[j] = wy8[j];

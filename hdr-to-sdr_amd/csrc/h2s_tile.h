@@ -349,7 +349,8 @@ template <int TRC, int TM, int DESAT, int LP, int DBG>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv, float qoff = 0.5f) {
+                                             long long di, float& oyv, float& ozv, float qoff = 0.5f,
+                                             float ydq = 0.0f) {
   constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
@@ -377,7 +378,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     const float B = enc(F.m709[6] * r + F.m709[7] * gg + F.m709[8] * bl);
     if (DBG == 3 || DBG == 4) dput(R, G, B);
     const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-    o.x = (16.0f + 219.0f * Y) * F.qscale + 0.5f;
+    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, 0.5f + ydq);
     o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
     o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
   } else {
@@ -422,6 +423,9 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+    // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
+    // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL)
+    o.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, ydq))));
     if (LP) {
       // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
       // Y'CbCr at depth q in the generic kernel's operation order; o = (luma
@@ -431,7 +435,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       const float B = __builtin_amdgcn_fmed3f(truncf(o.z * 255.0f), 0.0f, 255.0f) * F.inv255;
       if (DBG == 4) dput(R, G, B);
       const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-      o.x = (16.0f + 219.0f * Y) * F.qscale + 0.5f;
+      o.x = fmaf(16.0f + 219.0f * Y, F.qscale, 0.5f + ydq);
       o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
       o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
     }
@@ -443,7 +447,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
            w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
     }
   }
-  if (DBG == 5) dput(o.x - 0.5f, 4.0f * o.y, 4.0f * o.z);
+  if (DBG == 5) dput(o.x - 0.5f - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
   return eq_lds[(int)o.x];
 }
@@ -623,9 +627,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
     pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
   }
-  if (t < F.eq_n) eq_lds[t] = (uint16_t)(eq0 << F.shift_out);
-  for (int i = t + 256; i < F.eq_n; i += 256)  // native 10/12-bit tables
-    eq_lds[i] = (uint16_t)(__builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0) << F.shift_out);
+  // codes at the output depth: shift, or bit replication (h2s_expand;
+  // rep_rs = 8 - shift, or 31 for a plain shift: the 8-bit code >> 31 = 0)
+  if (t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
+  for (int i = t + 256; i < F.eq_n; i += 256) {  // native 10/12-bit tables
+    const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
+    eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
+  }
   if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (LP && F.lp_ipt) {
@@ -666,6 +674,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 #pragma unroll
   for (int i = 0; i < 4; i++)
     qo[i] = LP ? F.lp_qo + (F.lp_dith ? bayer16(xl + 8 * (i & 1), yl + 8 * (i >> 1)) : 0.5f) : 0.5f;
+  // S6 ordered dither (h2s_dither ORDERED, 8-bit quantiser): this lane's
+  // pixel is (xl, yl) mod 8 at every step (tile and step origins are
+  // multiples of 8), so its luma offset is one constant
+  const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
 
   for (;;) {
     // ---- commit this tile's registers to LDS ----
@@ -725,10 +737,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f);
-      const f3 o = {0.0f, oyv, ozv};
+          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
+      if (F.chr444) {
+        // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
+        // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
+        const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
+        if (py < F.H) F.chr444[(long long)py * F.chr_w + px] = make_float2(oyv * F.inv_c56, ozv * F.inv_c56);
+        continue;
+      }
       // chroma: 2x2 sums; the 4 lanes of a quad store the same value
-      const float su = quad_sum(o.y), sv = quad_sum(o.z);
+      const float su = quad_sum(oyv), sv = quad_sum(ozv);
       csb[oc] = su;
       csb[oc + CBH * CBW] = sv;
     }
@@ -752,7 +770,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
               oy_, lofs.sy, so + 2 * g.px0, NT);
       }
     }
-    if (t < 128) {
+    if (t < 128 && !F.chr444) {
       // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
       const int pl = __builtin_amdgcn_readfirstlane(t >> 6), rem = t & 63, r = rem >> 2, c = rem & 3;
       if (g.cy0 + r < F.ch) {
@@ -760,8 +778,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const float4 v0 = src[0], v1 = src[1];
         const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         unsigned code[8];
+        if (F.dither) {   // S6 ordered dither: sample (cx, cy) mod 8 = (k, r mod 8)
 #pragma unroll
-        for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias) << F.shift_out;
+          for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + (F.c_bias - 0.5f + dither_off(k, r)));
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) code[k] = (code[k] << F.shift_out) | (code[k] >> F.rep_rs);
         const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
         const int so = g.cy0 * (int)F.out_ls[1 + pl];
         if (F.out8)

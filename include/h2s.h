@@ -310,7 +310,10 @@ int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
  * Computed by the kernel h2s_process would use for this frame: the tile
  * kernel's own arithmetic (a debug instance of it) on the tile path, the
  * generic kernel otherwise (h2s_query_path; H2S_OPT_FAST_PATH = 0 forces the
- * generic one).  Synchronous. */
+ * generic one).  With peak_detect the curve uses the static peak (the
+ * parameters' resolved peak), not the context's smoothed state: the debug
+ * planes are a per-frame check of the arithmetic and leave that state
+ * untouched.  Synchronous. */
 int h2s_debug_float(h2s_ctx *ctx, const h2s_frames *in, int stage,
                     float *out_rgb, int out_location, void *hip_stream);
 

@@ -12,7 +12,8 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
-KERNEL = 'k_tile'
+# the C2 instance k_tile<PQ, Hable, RGB desat, CPU chain, DBG 0>
+KERNEL = 'k_tile<0, 5, 2, 0, 0>'
 
 for f in glob.glob(os.path.join(d, 'trace', '**', '*kernel_stats.csv'), recursive=True):
     print('## kernel stats', os.path.relpath(f, d))

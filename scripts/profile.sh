@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 evidence for the dominant kernel (k_process): kernel-trace stats
+# rocprofv3 evidence for the dominant kernel (k_tile, C2 instance): kernel-trace stats
 # plus PMC passes, each pass its own run (never combined with sys/runtime
 # traces).  Usage: bash scripts/profile.sh TAG [bench args...]
 set -u
@@ -9,7 +9,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--steps 6 --warmup 1 --cpu-seconds 0 --no-alt $*"
+ARGS="--steps 6 --warmup 1 --cpu-seconds 0 --no-alt --no-sharded $*"
 run() {  # run NAME rocprof-args...
   local name=$1; shift
   echo "=== $name"
