@@ -82,6 +82,10 @@ struct h2s_ctx {
   // device-wide synchronisation), then recycle them
   std::vector<hipEvent_t> pend, ev_free;
   hipEvent_t chr_ev = nullptr;   // after the last BICUBIC two-pass launch (d_chr scratch in use)
+  // set_params / set_lut copy and (re)allocate on this non-blocking stream
+  // (stream-ordered hipMallocAsync / hipFreeAsync for the lattices): no
+  // null-stream copy or hipFree, which would wait for the whole device
+  hipStream_t aux = nullptr;
   bool chr_pending = false;
   float2* d_chr = nullptr;       // BICUBIC chroma: one frame's per-pixel (Cb, Cr)
   unsigned* d_hist = nullptr;    // peak_detect percentile: per-frame PQ histograms
@@ -713,8 +717,12 @@ void h2s_destroy(h2s_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
   hipDeviceSynchronize();
-  if (c->d_lut) hipFree(c->d_lut);
-  if (c->d_lut_yuv) hipFree(c->d_lut_yuv);
+  if (c->aux) {  // the lattices are stream-ordered allocations of the context stream
+    if (c->d_lut) hipFreeAsync(c->d_lut, c->aux);
+    if (c->d_lut_yuv) hipFreeAsync(c->d_lut_yuv, c->aux);
+    hipStreamSynchronize(c->aux);
+    hipStreamDestroy(c->aux);
+  }
   if (c->d_eq) hipFree(c->d_eq);
   if (c->d_pq) hipFree(c->d_pq);
   if (c->d_pqi) hipFree(c->d_pqi);
@@ -754,6 +762,24 @@ static int drain_launches(h2s_ctx* c) {
   return 0;
 }
 
+static int aux_stream(h2s_ctx* c, hipStream_t* out) {
+  if (!c->aux) {
+    hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      c->aux = nullptr;
+      return hip_fail(c, e, "table stream");
+    }
+  }
+  *out = c->aux;
+  return 0;
+}
+
+// host -> device table copy on the context's own stream, waited for there
+static hipError_t table_copy(h2s_ctx* c, void* dst, const void* src, size_t bytes) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->aux);
+  return e == hipSuccess ? hipStreamSynchronize(c->aux) : e;
+}
+
 // record that this context queued work on stream s (after the launches)
 static int note_launch(h2s_ctx* c, hipStream_t s) {
   if (c->pend.size() >= 32) {   // recycle the events that have completed
@@ -789,21 +815,25 @@ int h2s_set_lut(h2s_ctx* c, const float* rgb, int n) {
   const size_t cnt = (size_t)n * n * n;
   std::vector<float4> host(cnt);
   for (size_t i = 0; i < cnt; i++) host[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.0f);
+  hipStream_t aux;
+  if (int rc = aux_stream(c, &aux)) return rc;
+  // a size change reallocates stream-ordered on the context's stream: a plain
+  // hipFree would wait for every stream on the device
   if (c->d_lut && c->lut_n != n) {
-    hipFree(c->d_lut);
+    hipFreeAsync(c->d_lut, aux);
     c->d_lut = nullptr;
-    if (c->d_lut_yuv) hipFree(c->d_lut_yuv);
+    if (c->d_lut_yuv) hipFreeAsync(c->d_lut_yuv, aux);
     c->d_lut_yuv = nullptr;
   }
   c->lut_yuv_scale = -1.0f;
   if (!c->d_lut) {
-    hipError_t e = hipMalloc((void**)&c->d_lut, cnt * sizeof(float4));
+    hipError_t e = hipMallocAsync((void**)&c->d_lut, cnt * sizeof(float4), aux);
     if (e != hipSuccess) {
       c->d_lut = nullptr;
       return fail(c, H2S_E_OOM, "LUT device allocation failed");
     }
   }
-  hipError_t e = hipMemcpy(c->d_lut, host.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  hipError_t e = table_copy(c, c->d_lut, host.data(), cnt * sizeof(float4));
   if (e != hipSuccess) return hip_fail(c, e, "LUT upload");
   c->lut_n = n;
   return 0;
@@ -816,6 +846,8 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   if (rc) return rc;
   DeviceGuard g(c->device);
   if ((rc = drain_launches(c))) return rc;
+  hipStream_t aux;
+  if ((rc = aux_stream(c, &aux))) return rc;
   std::vector<uint16_t> eq;
   KParams k;
   resolve(p, &k, &eq);
@@ -826,7 +858,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
       return fail(c, H2S_E_OOM, "eq table allocation failed");
     }
   }
-  hipError_t e = hipMemcpy(c->d_eq, eq.data(), eq.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+  hipError_t e = table_copy(c, c->d_eq, eq.data(), eq.size() * sizeof(uint16_t));
   if (e != hipSuccess) return hip_fail(c, e, "eq table upload");
   {
     std::vector<float4> pq;
@@ -837,7 +869,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
       c->d_pq = nullptr;
       return fail(c, H2S_E_OOM, "PQ table allocation failed");
     }
-    if ((e = hipMemcpy(c->d_pq, pq.data(), pq.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
+    if ((e = table_copy(c, c->d_pq, pq.data(), pq.size() * sizeof(float4))) != hipSuccess)
       return hip_fail(c, e, "PQ table upload");
     if (!c->d_pqi) {
       std::vector<float4> pqi;
@@ -846,7 +878,7 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
         c->d_pqi = nullptr;
         return fail(c, H2S_E_OOM, "PQ encode table allocation failed");
       }
-      if ((e = hipMemcpy(c->d_pqi, pqi.data(), pqi.size() * sizeof(float4), hipMemcpyHostToDevice)) != hipSuccess)
+      if ((e = table_copy(c, c->d_pqi, pqi.data(), pqi.size() * sizeof(float4))) != hipSuccess)
         return hip_fail(c, e, "PQ encode table upload");
     }
   }
@@ -973,10 +1005,11 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
 static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
   if (c->d_lut_yuv && c->lut_yuv_scale == k.qscale && c->lut_yuv_rgb == k.rgba8) return 0;
   const size_t cnt = (size_t)c->lut_n * c->lut_n * c->lut_n;
-  if (!c->d_lut_yuv) {
-    const size_t m = (size_t)c->lut_n - 1;
-    (void)m;
-    hipError_t e = hipMalloc((void**)&c->d_lut_yuv, cnt * 3 * sizeof(float) + 16);
+  if (!c->d_lut_yuv) {  // beside d_lut: stream-ordered on the context stream, complete before s uses it
+    hipStream_t aux;
+    if (int rc = aux_stream(c, &aux)) return rc;
+    hipError_t e = hipMallocAsync((void**)&c->d_lut_yuv, cnt * 3 * sizeof(float) + 16, aux);
+    if (e == hipSuccess) e = hipStreamSynchronize(aux);
     if (e != hipSuccess) {
       c->d_lut_yuv = nullptr;
       return fail(c, H2S_E_OOM, "YUV lattice allocation failed");

@@ -9,7 +9,7 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
 export H2S_FLOAT_REPORT=$OUT/float_report.jsonl
-export H2S_FLOOR_ONLY_MAX=${H2S_FLOOR_ONLY_MAX:-0.02}
+# (H2S_FLOOR_ONLY_MAX, when set, overrides the per-kind floor-only bounds)
 rm -f "$H2S_FLOAT_REPORT"
 timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_STOP:--x} -q --timeout 300 --timeout-method thread "$@" \
   > "$OUT/pytest_gpu.log" 2>&1

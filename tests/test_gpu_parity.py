@@ -230,9 +230,12 @@ FLOAT_CFGS = {
 # Pixels excluded as ill-conditioned (see check_float_stage) and values that
 # pass only because of the absolute floor, per (kernel, config, content,
 # stage), are written to $H2S_FLOAT_REPORT (one JSON line each) when set, and
-# bounded here: the floor may carry at most FLOOR_ONLY_MAX of the values that
-# would otherwise fail 1e-3 relative.
-FLOOR_ONLY_MAX = 0.02
+# bounded here per content: the share of values that fail 1e-3 relative and
+# pass through a floor (DESIGN.md §2 holds the measured table).  The ramp
+# sweeps PQ 0 -> 1 along x, so ~6 % of its samples lie below 0.02 nits, where
+# the 2e-7 npl floor of the EOTF table's first segment exceeds 1e-3
+# relative; 'edges' puts a third of its codes in the sub-black band.
+FLOOR_ONLY_MAX = {'ramp': 0.06, 'edges': 0.05, 'uniform': 0.03, 'smooth': 0.02}
 
 
 def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
@@ -262,13 +265,13 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     # round-1 floor of 1e-5, except at stage 4, where the lattice's gamut-clip
     # bend next to black multiplies the PQ pow's float32 disagreement
     # (~4e-5 relative at stage 1, any two implementations) by its slope:
-    # measured 5.0e-5 absolute at most ('uniform', R'G'B' ~0.011), floor 1e-4.
+    # measured 1.75e-4 absolute at most (C4 native, 'ramp', R'G'B' 0.031), floor 3e-4.
     if kernel == 'k_tile':
         floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
     else:
         # stage 5 is in code units at depth q: the stage-4 floor through the
         # Y'CbCr rows (224 codes per unit at 8 bits)
-        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-4, 5: 224 * (1 << (q - 8)) * 1e-4}[stage]
+        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 3e-4, 5: 224 * (1 << (q - 8)) * 3e-4}[stage]
     got = got.astype(np.float64)
     with np.errstate(invalid='ignore'):
         err = np.abs(got - want)
@@ -363,7 +366,7 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {float(np.max(floor)):g} '
                            f'({int(skip.sum())} ill-conditioned pixels excluded); worst: want '
                            f'{float(want.flat[i]):.6g} got {float(got.flat[i]):.6g}')
-    bound = float(os.environ.get('H2S_FLOOR_ONLY_MAX', FLOOR_ONLY_MAX))   # (a survey run may lift it)
+    bound = float(os.environ.get('H2S_FLOOR_ONLY_MAX', FLOOR_ONLY_MAX[kind]))   # (a survey run may lift it)
     assert report['floor_only_frac'] <= bound, (
         f'{report["floor_only_frac"]:.2%} of values pass only through the floor (bound {bound:.0%})')
     return report

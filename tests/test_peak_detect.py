@@ -127,7 +127,9 @@ def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline, mo
     tm.close()
     got = np.concatenate(got).astype(np.int64)
     want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
-    assert len(set(round(p, 3) for p in peaks)) >= 3          # the peak really moves
+    # the peak really moves (under vf_libplacebo's defaults the darker frames
+    # sit at the minimum peak, 1.0 x the 203-nit white)
+    assert len(set(round(p, 3) for p in peaks)) >= (3 if model == 'round2' else 2)
     assert state['frames'] == 6 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
     assert_close_int(params, got, want.astype(np.int64), W, H)
 
