@@ -51,10 +51,11 @@ def test_bicubic_chroma_matches_oracle(tm, W, H, bits_out, kind):
     assert bic == (_abi.PATH_TWO_PASS if box == _abi.PATH_GENERIC else box)
 
 
-@pytest.mark.parametrize('W,H,bits_out', [(256, 64, 10), (200, 96, 8)])
+@pytest.mark.parametrize('W,H,bits_out', [(256, 64, 10), (352, 34, 8)])    # whole tiles; tiles + tail
 def test_bicubic_tile_pass_equals_generic(tm, W, H, bits_out):
     params = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2, bits_out=bits_out, chroma_filter='bicubic')
     tile, _, _ = run_both(tm, params, 'smooth', W, H, nframes=3)
+    assert _path(tm, params, W, H) == (_abi.PATH_TILE if W % 64 == 0 else _abi.PATH_TILE_TAIL)
     tm.set_option(_abi.OPT_FAST_PATH, 0)
     try:
         gen, _, _ = run_both(tm, params, 'smooth', W, H, nframes=3)
@@ -111,7 +112,7 @@ def test_bit_replication_matches_oracle(tm, bits_out):
     assert np.array_equal(got, (v8 << s) | (v8 >> (8 - s)))           # every code is a replication
 
 
-@pytest.mark.parametrize('W,H', [(128, 64), (200, 96)])                   # whole tiles; tiles + generic tail
+@pytest.mark.parametrize('W,H', [(128, 64), (352, 34)])                   # whole tiles; tiles + generic tail (16-B rows)
 @pytest.mark.parametrize('kw', [dict(dither='ordered', bits_out=8), dict(dither='ordered', bits_out=10, gamma=1.4),
                                 dict(expand='replicate', bits_out=10), dict(expand='replicate', bits_out=12),
                                 dict(dither='ordered', expand='replicate', bits_out=12)])
