@@ -1198,7 +1198,8 @@ static int choose_path(const h2s_ctx* c, const KParams& k, const h2s_frames* din
 }
 
 static int ensure_chr(h2s_ctx* c, const KParams& k) {
-  const size_t need = (size_t)k.W * k.H;
+  // whole 32-row tiles: k_tile writes the rows of its bottom tile past H
+  const size_t need = (size_t)k.W * (size_t)((k.H + h2s::TBH - 1) / h2s::TBH * h2s::TBH);
   if (need <= c->chr_cap) return 0;
   if (c->d_chr) hipFree(c->d_chr);
   c->d_chr = nullptr;

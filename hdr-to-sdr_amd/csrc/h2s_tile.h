@@ -151,7 +151,8 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // tone_ipt.
 template <int TRC, int TM, int DESAT, int LP>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
-                                     const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s) {
+                                     const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s,
+                                     float hable_kb) {
   if (LP && TM >= 4 && TM <= 6) {
     // libplacebo's reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = the
     // target white; oracle lp_norm_curve), on the IPT intensity or as the
@@ -312,7 +313,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
     // terms cancel: d*e*15 = d*f), so hable(x)/x = (0.14 x + 1/60) / D:
     // one reciprocal, no cancellation, and sig drops out of the gain
     const float den = fmaf(sig, fmaf(sig, 0.15f, 0.50f), 0.06f);
-    k = fmaf(sig, F.hable_ka, F.hable_kb) * frcp(den);
+    k = fmaf(sig, F.hable_ka, hable_kb) * frcp(den);   // (kb in a VGPR: one scalar operand per VOP3)
   } else {
     const float m = F.mob_k * (sig + F.mob_a) * frcp((sig + F.mob_b) * sig);
     k = sig <= F.mob_j ? 1.0f : m;
@@ -338,6 +339,7 @@ struct StepK {
   float stride_g, stride_b;       // lattice byte strides (as floats)
   int og, ob, ocr, ocg, ocb;      // corner byte offsets
   float log2_nm1, x_max;
+  float hable_kb;                 // F.hable_kb (Hable instances)
 };
 
 // One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
@@ -349,8 +351,7 @@ template <int TRC, int TM, int DESAT, int LP, int DBG>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv, float qoff = 0.5f,
-                                             float ydq = 0.0f) {
+                                             long long di, float& oyv, float& ozv, float qoff, float ydq) {
   constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
@@ -362,7 +363,8 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
   };
   if (DBG == 1) dput(r, gg, bl);
-  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb));
+  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb),
+                           K.hable_kb);
   if (DBG == 2) dput(r, gg, bl);
   f3 o;
   if (LP && F.lut_off) {
@@ -487,7 +489,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint8_t* base
 // one tile's global loads, held in registers between issue and the LDS commit
 struct TileRegs {
   uint4 ya, ua;     // luma chunk; chroma chunk of plane pc (threads tc < 72)
-  unsigned uh;      // the chroma chunk's right-halo sample
+  uint16_t uh;      // the chroma chunk's right-halo sample
 };
 
 struct TileGeo {
@@ -556,39 +558,128 @@ __device__ __forceinline__ LaneOfs lane_ofs(const FastParams& F, int t) {
 // origin; border tiles clamp per lane.  The chroma registers of threads >= 72
 // are left undefined (never committed).
 __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo& g, int t, const LaneOfs& L) {
+  // Every thread issues exactly one load of each kind whatever the tile: the
+  // offsets are chosen per case and the loads follow the merge; threads
+  // without a chroma chunk read out of range, which returns 0 and fetches
+  // nothing
   const __amdgpu_buffer_rsrc_t iy = plane_rsrc(F.in[0] + g.f * F.in_fp[0], F.in_bytes[0]);
   const int yr = t >> 3, yc = t & 7;
   TileRegs r;
-  if (g.py0 + TBH <= F.H)   // block-uniform
-    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                         iy, L.y, g.py0 * (int)F.in_ls[0] + 2 * g.px0, NT));
-  else
-    r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                         iy, (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), 0, NT));
-  const int pc = __builtin_amdgcn_readfirstlane(t >> 7), tc = t & 127;
-  if (tc < 72) {
-    const __amdgpu_buffer_rsrc_t ic = plane_rsrc(F.in[1 + pc] + g.f * F.in_fp[1 + pc], F.in_bytes[1 + pc]);
-    const int ls = (int)F.in_ls[1 + pc];
-    if (g.cy0 >= 1 && g.cy0 + CBH + 1 <= F.ch && g.cx0 + CBW + 1 <= F.cw) {   // block-uniform
-      const int so = (g.cy0 - 1) * ls + 2 * g.cx0;
-      r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, L.u, so, NT));
-      r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, L.u + 16, so, 0);
-    } else {
-      const int clr = tc >> 2, ccx = tc & 3;
-      const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
-      const int hx = 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
-      r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, row * ls + 2 * (g.cx0 + 8 * ccx), 0, NT));
-      r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, row * ls + hx, 0, 0);
-    }
+  int vy, sy;
+  if (g.py0 + TBH <= F.H) {   // block-uniform
+    vy = L.y, sy = g.py0 * (int)F.in_ls[0] + 2 * g.px0;
+  } else {
+    vy = (g.py0 + yr < F.H ? g.py0 + yr : F.H - 1) * (int)F.in_ls[0] + 2 * (g.px0 + 8 * yc), sy = 0;
   }
+  r.ya = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(iy, vy, sy, NT));
+  const int pc = __builtin_amdgcn_readfirstlane(t >> 7), tc = t & 127;
+  const __amdgpu_buffer_rsrc_t ic = plane_rsrc(F.in[1 + pc] + g.f * F.in_fp[1 + pc], F.in_bytes[1 + pc]);
+  const int ls = (int)F.in_ls[1 + pc];
+  int vc, vh, sc;
+  if (g.cy0 >= 1 && g.cy0 + CBH + 1 <= F.ch && g.cx0 + CBW + 1 <= F.cw) {   // block-uniform
+    vc = L.u, vh = L.u + 16, sc = (g.cy0 - 1) * ls + 2 * g.cx0;
+  } else {
+    const int clr = tc >> 2, ccx = tc & 3;
+    const int row = chroma_edge_at(g.cy0 - 1 + clr, F.ch, F.chroma_edge);
+    vc = row * ls + 2 * (g.cx0 + 8 * ccx);
+    vh = row * ls + 2 * chroma_edge_at(g.cx0 + 8 * ccx + 8, F.cw, F.chroma_edge);
+    sc = 0;
+  }
+  if (tc >= 72) vc = vh = 0x7FFFFFF0;
+  r.ua = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ic, vc, sc, NT));
+  r.uh = __builtin_amdgcn_raw_buffer_load_b16(ic, vh, sc, 0);
   return r;
+}
+
+// staging and store helpers of k_tile
+// 8 luma samples -> Y*ys + y_off floats at (row, 8 col8)
+__device__ __forceinline__ void stage_luma(float* yin, uint4 a, int row, int col8, float ysc, float yoff) {
+  float v[8];
+  unpack8(a, v);
+  float* d = yin + row * YST + 8 * col8;
+  *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
+  *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
+}
+// horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
+// h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float.  tt: chunk index
+// (row tt >> 2, 8-sample chunk tt & 3) of the tile's 18 x 4 chroma chunks
+__device__ __forceinline__ void stage_chroma(float* plane, uint4 a, unsigned h, int tt, float cmid) {
+  float v[9];
+  unpack8(a, v);
+  v[8] = (float)h;
+#pragma unroll
+  for (int k = 0; k < 9; k++) v[k] -= cmid;
+  float* d = plane + (tt >> 2) * HST + 16 * (tt & 3);
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    *reinterpret_cast<float4*>(d + 4 * k) =
+        make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
+}
+// luma codes of tile row r, chunk c (8 pixels), packed for one 16-byte (u16)
+// / 8-byte (u8: .xy) store
+__device__ __forceinline__ u4v read_luma(const FastParams& F, const float* yin, int r, int c) {
+  const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
+  const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
+  if (F.out8)
+    return u4v{a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24), 0u, 0u};
+  return u4v{a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16)};
+}
+__device__ __forceinline__ void put_luma(const FastParams& F, const TileGeo& g, u4v v, int r, int vo, int so) {
+  if (g.py0 + r >= F.H) return;
+  const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
+  so += g.py0 * (int)F.out_ls[0];
+  if (F.out8)
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oy_, vo, so + g.px0, NT);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, oy_, vo, so + 2 * g.px0, NT);
+}
+// chroma plane pl, row r, chunk c (8 samples): ((c0 + c1) + (c2 + c3)) + bias,
+// quantised once per sample, packed as read_luma
+__device__ __forceinline__ u4v read_chroma(const FastParams& F, const float* csum, int pl, int r, int c) {
+  const float4* src = reinterpret_cast<const float4*>(csum + pl * (CBH * CBW) + r * CBW + 8 * c);
+  const float4 v0 = src[0], v1 = src[1];
+  const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  unsigned code[8];
+  if (F.dither) {   // S6 ordered dither: sample (cx, cy) mod 8 = (k, r mod 8)
+#pragma unroll
+    for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + (F.c_bias - 0.5f + dither_off(k, r)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias);
+  }
+  if (F.rep_rs == 31) {   // plain shift (block-uniform); else bit replication (h2s_expand)
+#pragma unroll
+    for (int k = 0; k < 8; k++) code[k] <<= F.shift_out;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) code[k] = (code[k] << F.shift_out) | (code[k] >> F.rep_rs);
+  }
+  if (F.out8)
+    return u4v{code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
+               code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24), 0u, 0u};
+  return u4v{code[0] | (code[1] << 16), code[2] | (code[3] << 16), code[4] | (code[5] << 16), code[6] | (code[7] << 16)};
+}
+__device__ __forceinline__ void put_chroma(const FastParams& F, const TileGeo& g, u4v v, int pl, int r, int vo) {
+  if (g.cy0 + r >= F.ch) return;
+  const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
+  const int so = g.cy0 * (int)F.out_ls[1 + pl];
+  if (F.out8)
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oc_, vo, so + g.cx0, NT);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, oc_, vo, so + 2 * g.cx0, NT);
 }
 
 // Each block walks F.tpb consecutive tiles (XCD-remapped, so neighbouring
 // tiles and their lattice cells share one XCD's L2).  The loads of tile i+1
 // are issued before tile i is computed, so after the first tile the block no
 // longer waits on HBM latency.  Per tile: commit registers -> LDS, prefetch,
-// barrier, 8 compute steps, barrier, store, barrier.
+// barrier, 8 compute steps, barrier, store, barrier.  (A fifth wave doing all
+// of the frame I/O, so that the compute waves' gathers never wait behind the
+// prefetch in the shared vector-memory counter, measured 1.5x slower: its
+// serial store + commit phase idles the four compute waves;
+// profiles/r03/ablations/io_wave*.  Issuing the stores of tile i-1 and the
+// loads of tile i+1 inside step 7, behind its gathers, measured 3-5 % slower:
+// profiles/r03/ablations/late_io*.)
 // DBG (debug instances only, never launched by h2s_process): 1..5 = also
 // write that h2s_stage's three float planes for frame 0 to F.dbg (W x H each)
 // from this kernel's own arithmetic — stage 4 blends the float4 RGB lattice
@@ -611,6 +702,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
 
   const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
   const unsigned ntiles = F.nbx * F.nby * F.nframes;
   unsigned tile = (unsigned)fxcd_remap(blockIdx.x, gridDim.x) * (unsigned)F.tpb;
   const unsigned tend = tile + (unsigned)F.tpb < ntiles ? tile + (unsigned)F.tpb : ntiles;
@@ -645,9 +737,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block
   // (2w + (s&1), s>>1); lane = pixel (quad q = lane>>2 in a 4x4 quad grid,
   // position lane&3 in the quad) ----
-  const int lane = t & 63, w = t >> 6;
   const int qx = (lane >> 2) & 3, qy = lane >> 4, pxl = lane & 1, pyl = (lane >> 1) & 1;
-  const int xl = 16 * w + 2 * qx + pxl, yl = 2 * qy + pyl;                 // step (0,0) pixel
+  const int xl = 16 * w + 2 * qx + pxl, yl = 2 * qy + pyl;           // step (0,0) pixel
   const float* ybase = yin + yl * YST + xl;
   // vertical pass (centre siting): 3 x row cy + row cy-1 (top) / cy+1 (bottom)
   const float* h0 = hrow[0] + (qy + 1) * HST + xl;
@@ -666,7 +757,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
-  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max};
+  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
+                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb};
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
@@ -679,49 +771,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   // multiples of 8), so its luma offset is one constant
   const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
 
-  for (;;) {
-    // ---- commit this tile's registers to LDS ----
-    if (F.in_mask2 != 0xFFFFFFFFu) {   // h2s_lp_p010 TRUNCATE (block-uniform)
-      cur.ya.x &= F.in_mask2, cur.ya.y &= F.in_mask2, cur.ya.z &= F.in_mask2, cur.ya.w &= F.in_mask2;
-      cur.ua.x &= F.in_mask2, cur.ua.y &= F.in_mask2, cur.ua.z &= F.in_mask2, cur.ua.w &= F.in_mask2;
-      cur.uh &= F.in_mask2;
-    }
-    {
-      float v[8];
-      unpack8(cur.ya, v);
-      float* d = yin + (t >> 3) * YST + 8 * (t & 7);
-      *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
-      *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
-    }
-    if ((t & 127) < 72) {
-      // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
-      // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float
-      auto put = [&](const uint4 a, unsigned h, float* plane, int tt) {
-        float v[9];
-        unpack8(a, v);
-        v[8] = (float)h;
-#pragma unroll
-        for (int k = 0; k < 9; k++) v[k] -= cmid;
-        float* d = plane + (tt >> 2) * HST + 16 * (tt & 3);
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          *reinterpret_cast<float4*>(d + 4 * k) =
-              make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
-      };
-      put(cur.ua, cur.uh, hrow[__builtin_amdgcn_readfirstlane(t >> 7)], t & 127);
-    }
-    const TileGeo g = geo;
+  // the 8 compute steps of one tile (compute waves)
+  auto steps = [&](const TileGeo& g) {
     // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
     // frame, read through the scalar cache; the frame index is block-uniform)
     CurveConsts cv = F;
     if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
-    const bool more = tile + 1 < tend;   // block-uniform
-    if (more) {
-      tile_next(F, geo);
-      cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
-    }
-    __syncthreads();
-
     const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
@@ -741,8 +796,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       if (F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
+        // (the scratch has whole tiles of rows: rows past F.H are written, never read)
         const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
-        if (py < F.H) F.chr444[(long long)py * F.chr_w + px] = make_float2(oyv * F.inv_c56, ozv * F.inv_c56);
+        F.chr444[(long long)py * F.chr_w + px] = make_float2(oyv * F.inv_c56, ozv * F.inv_c56);
         continue;
       }
       // chroma: 2x2 sums; the 4 lanes of a quad store the same value
@@ -750,57 +806,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       csb[oc] = su;
       csb[oc + CBH * CBW] = sv;
     }
+  };
+  auto mask_in = [&](uint4& a) {   // h2s_lp_p010 TRUNCATE (block-uniform)
+    a.x &= F.in_mask2, a.y &= F.in_mask2, a.z &= F.in_mask2, a.w &= F.in_mask2;
+  };
+
+  const int pl = __builtin_amdgcn_readfirstlane(t >> 6) & 1, rem = t & 63;   // chroma store role (t < 128)
+  const bool cst = t < 128 && !F.chr444;
+  for (;;) {
+    // ---- commit this tile's registers to LDS ----
+    if (F.in_mask2 != 0xFFFFFFFFu) {   // h2s_lp_p010 TRUNCATE (block-uniform)
+      mask_in(cur.ya), mask_in(cur.ua);
+      cur.uh &= F.in_mask2;
+    }
+    stage_luma(yin, cur.ya, t >> 3, t & 7, ysc, yoff);
+    if ((t & 127) < 72) stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
+    const TileGeo g = geo;
+    const bool more = tile + 1 < tend;   // block-uniform
+    if (more) {
+      tile_next(F, geo);
+      cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
+    }
+    __syncthreads();
+    steps(g);
     __syncthreads();
 
     // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
-    {
-      const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
-      const int r = t >> 3, c = t & 7;
-      if (g.py0 + r < F.H) {
-        const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
-        const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
-        const int so = g.py0 * (int)F.out_ls[0];
-        if (F.out8)
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u2v, make_uint2(a.x | (a.y << 8) | (a.z << 16) | (a.w << 24), b.x | (b.y << 8) | (b.z << 16) | (b.w << 24))),
-              oy_, lofs.sy, so + g.px0, NT);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u4v, make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16))),
-              oy_, lofs.sy, so + 2 * g.px0, NT);
-      }
-    }
-    if (t < 128 && !F.chr444) {
-      // chroma: ((c0 + c1) + (c2 + c3)) + bias, quantised once per sample
-      const int pl = __builtin_amdgcn_readfirstlane(t >> 6), rem = t & 63, r = rem >> 2, c = rem & 3;
-      if (g.cy0 + r < F.ch) {
-        const float4* src = reinterpret_cast<const float4*>(csum[pl] + r * CBW + 8 * c);
-        const float4 v0 = src[0], v1 = src[1];
-        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        unsigned code[8];
-        if (F.dither) {   // S6 ordered dither: sample (cx, cy) mod 8 = (k, r mod 8)
-#pragma unroll
-          for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + (F.c_bias - 0.5f + dither_off(k, r)));
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) code[k] = (unsigned)(int)(vv[k] + F.c_bias);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) code[k] = (code[k] << F.shift_out) | (code[k] >> F.rep_rs);
-        const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
-        const int so = g.cy0 * (int)F.out_ls[1 + pl];
-        if (F.out8)
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u2v, make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
-                                                 code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24))),
-              oc_, lofs.sc, so + g.cx0, NT);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u4v, make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
-                                                 code[4] | (code[5] << 16), code[6] | (code[7] << 16))),
-              oc_, lofs.sc, so + 2 * g.cx0, NT);
-      }
-    }
+    put_luma(F, g, read_luma(F, yin, t >> 3, t & 7), t >> 3, lofs.sy, 0);
+    if (cst) put_chroma(F, g, read_chroma(F, csum[0], pl, rem >> 2, rem & 3), pl, rem >> 2, lofs.sc);
     if (!more) break;
     ++tile;
     __syncthreads();   // the store phase has read yin / csum before they are refilled
