@@ -60,6 +60,31 @@ def _lattice_max_step(n):
     return max(float(np.abs(np.diff(a, axis=ax)).max()) for ax in range(3))
 
 
+def lattice_slope(n, s3):
+    """Per pixel, output channel and input axis: the largest |corner
+    difference| along that axis over the lattice cell that holds the stage-3
+    coordinates s3 (3, H, W) in [0, 1], times (n - 1): a bound on the
+    tetrahedral interpolant's partial derivatives there (it is linear on each
+    tetrahedron, with slopes equal to corner differences).  Returns (c, a, H, W)."""
+    a = lattice(n).reshape(n, n, n, 3).astype(np.float64)          # [b][g][r][c]
+    x = np.clip(np.nan_to_num(s3, nan=0.0), 0.0, 1.0) * (n - 1)
+    i = np.minimum(np.floor(x).astype(np.int64), n - 2)
+    ir, ig, ib = i[0], i[1], i[2]
+    out = np.zeros((3, 3) + s3.shape[1:])
+    for ax in range(3):          # 0 = r, 1 = g, 2 = b
+        best = np.zeros((3,) + s3.shape[1:])
+        for db in (0, 1):
+            for dg in (0, 1):
+                for dr in (0, 1):
+                    if (dr, dg, db)[ax]:
+                        continue
+                    lo = a[ib + db, ig + dg, ir + dr]
+                    hi = a[ib + db + (ax == 2), ig + dg + (ax == 1), ir + dr + (ax == 0)]
+                    best = np.maximum(best, np.moveaxis(np.abs(hi - lo), -1, 0))
+        out[:, ax] = best * (n - 1)
+    return out
+
+
 def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
     """Chroma: |diff| <= one quantisation step.  Luma: eq runs after the
     quantiser, so the bound is +-1 step *before* eq: got must lie between
@@ -262,16 +287,14 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     q = oracle.quant_bits(op)
     # The 6e-4 floor on stages 3/4 belongs to k_tile's PQ EOTF table (its first
     # segment); the generic kernel evaluates the EOTF with powf and keeps the
-    # round-1 floor of 1e-5, except at stage 4, where the lattice's gamut-clip
-    # bend next to black multiplies the PQ pow's float32 disagreement
-    # (~4e-5 relative at stage 1, any two implementations) by its slope:
-    # measured 1.75e-4 absolute at most (C4 native, 'ramp', R'G'B' 0.031), floor 3e-4.
+    # round-1 floor of 1e-5 on every stage (stage 5 in code units at depth q:
+    # through the Y'CbCr rows, 224 codes per unit at 8 bits).  At stages 4/5
+    # the lattice's slope multiplies the stage-3 disagreement: that term is
+    # carried as conditioning (lattice_slope below), not as a floor.
     if kernel == 'k_tile':
         floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
     else:
-        # stage 5 is in code units at depth q: the stage-4 floor through the
-        # Y'CbCr rows (224 codes per unit at 8 bits)
-        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 3e-4, 5: 224 * (1 << (q - 8)) * 3e-4}[stage]
+        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-5, 5: 224 * (1 << (q - 8)) * 1e-5}[stage]
     got = got.astype(np.float64)
     with np.errstate(invalid='ignore'):
         err = np.abs(got - want)
@@ -321,6 +344,21 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens
     rel = (1e-3 + 4e-5 * kappa[None]) * np.abs(want)
     tol = rel + floor
+    if kernel != 'k_tile' and stage in (4, 5) and params.lut_enabled and params.resolved_pipeline() != 'libplacebo':
+        # The PQ pow in float32 disagrees by up to ~4e-5 relative between any
+        # two implementations (stage 1, see kappa above); x^(1/2.4) divides a
+        # relative error by 2.4 and desaturation above its threshold amplifies
+        # it by kappa, so a stage-3 coordinate carries d3 = (4e-5 / 2.4)(1 +
+        # kappa) s3 + the stage-3 floor; the tetrahedral interpolant passes it
+        # on times its local slope.  This bounds the lattice's gamut-clip
+        # bend next to black (round 2: 1.75e-4 absolute at R'G'B' 0.031 on
+        # C4 native 'ramp'), where a floor of 3e-4 used to stand in for it.
+        s3 = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 3).astype(np.float64)
+        d3 = (4e-5 / 2.4) * (1.0 + kappa[None]) * np.abs(np.nan_to_num(s3)) + 1e-5
+        cond4 = np.einsum('cahw,ahw->chw', lattice_slope(65, s3), d3)
+        if stage == 5:
+            cond4 = 224 * (1 << (q - 8)) * cond4.max(axis=0, keepdims=True)
+        tol = tol + np.nan_to_num(cond4, nan=0.0)
     if params.resolved_pipeline() == 'libplacebo' and params.lp_tone == 'ipt' and stage in (2, 3):
         # the IPT form's LMS -> RGB rows (absolute sums up to 5.3) turn the
         # LMS values' relative error into an absolute error on channels they
@@ -340,6 +378,7 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     with np.errstate(invalid='ignore', divide='ignore'):
         beyond_rel = keep & (err > rel)                        # would fail 1e-3 (+ kappa term) alone
         floor_only = beyond_rel & (err <= tol)                 # ... and pass through a floor / conditioning term
+        # (for the generic kernel's stages 4/5 that share includes the lattice-slope term)
         relerr = np.where(keep & ~beyond_rel & (np.abs(want) > 0), err / np.abs(want), 0.0)
     report = dict(kernel=kernel, cfg=cfg, kind=kind, stage=stage, values=int(want.size),
                   excluded_px=int(skip.sum()), excluded_frac=float(skip.mean()),
