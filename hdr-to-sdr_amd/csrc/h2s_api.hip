@@ -55,6 +55,7 @@ struct h2s_ctx {
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
+  float4* d_hlg = nullptr; // HLG inverse-OETF cubic segments (fast path, CPU chain)
   float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
@@ -503,14 +504,10 @@ void build_pqi_table(std::vector<float4>* out) {
 // PQ EOTF x scale as PQ_NSEG cubic segments: per segment, the cubic through
 // the exact (double) EOTF at the 4 Chebyshev nodes of the segment.  Measured
 // max relative error 1.2e-7 for E > 0.05 (float32 evaluation).
-void build_pq_table(double scale, std::vector<float4>* out) {
-  const double m1 = 2610.0 / 16384, m2 = 2523.0 / 32, c1 = 3424.0 / 4096, c2 = 2413.0 / 128, c3 = 2392.0 / 128;
-  auto eotf = [&](double e) {
-    if (!(e > 0)) return 0.0;
-    const double xp = pow(e, 1.0 / m2);
-    const double num = fmax(xp - c1, 0.0), den = c2 - c3 * xp;
-    return den > 0 ? pow(num / den, 1.0 / m1) * scale : HUGE_VAL;
-  };
+// cubic segments of f over E in [i, i+1) / PQ_SEG, i < PQ_NSEG, interpolating
+// f at the four Chebyshev nodes of each segment (k_tile's pq_z layout)
+template <class Fn>
+static void build_seg_table(const Fn& eotf, std::vector<float4>* out) {
   double t[4];
   for (int k = 0; k < 4; k++) t[k] = (1.0 - cos((2 * k + 1) * M_PI / 8.0)) / 2.0;
   out->resize(h2s::PQ_NSEG);
@@ -537,6 +534,28 @@ void build_pq_table(double scale, std::vector<float4>* out) {
     if (i == 0) c[0] = 0.0;  // E = 0 maps to exactly 0, as zimg's x > 0 test
     (*out)[i] = make_float4((float)c[3], (float)c[2], (float)c[1], (float)c[0]);
   }
+}
+
+void build_pq_table(double scale, std::vector<float4>* out) {
+  const double m1 = 2610.0 / 16384, m2 = 2523.0 / 32, c1 = 3424.0 / 4096, c2 = 2413.0 / 128, c3 = 2392.0 / 128;
+  build_seg_table([&](double e) {
+    if (!(e > 0)) return 0.0;
+    const double xp = pow(e, 1.0 / m2);
+    const double num = fmax(xp - c1, 0.0), den = c2 - c3 * xp;
+    return den > 0 ? pow(num / den, 1.0 / m1) * scale : HUGE_VAL;
+  }, out);
+}
+
+// zimg arib_b67_inverse_oetf (k_tile's HLG input on the CPU chain; the OOTF
+// follows in the kernel): E^2 / 3 up to 1/2, (exp((E - c) / a) + b) / 12
+// above; 1/2 is a segment boundary, so every segment interpolates one smooth
+// branch (the quadratic one exactly)
+void build_hlg_table(std::vector<float4>* out) {
+  const double a = 0.17883277, b = 0.28466892, c = 0.55991073;
+  build_seg_table([&](double e) {
+    if (!(e > 0)) return 0.0;
+    return e <= 0.5 ? e * e / 3.0 : (exp((e - c) / a) + b) / 12.0;
+  }, out);
 }
 
 bool aligned(const void* p, long long a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
@@ -725,6 +744,7 @@ void h2s_destroy(h2s_ctx* c) {
   }
   if (c->d_eq) hipFree(c->d_eq);
   if (c->d_pq) hipFree(c->d_pq);
+  if (c->d_hlg) hipFree(c->d_hlg);
   if (c->d_pqi) hipFree(c->d_pqi);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
@@ -881,6 +901,16 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
       if ((e = table_copy(c, c->d_pqi, pqi.data(), pqi.size() * sizeof(float4))) != hipSuccess)
         return hip_fail(c, e, "PQ encode table upload");
     }
+    if (!c->d_hlg && p->transfer_in == H2S_TRC_HLG) {   // parameter-independent: built once
+      std::vector<float4> hlg;
+      build_hlg_table(&hlg);
+      if ((e = hipMalloc((void**)&c->d_hlg, hlg.size() * sizeof(float4))) != hipSuccess) {
+        c->d_hlg = nullptr;
+        return fail(c, H2S_E_OOM, "HLG table allocation failed");
+      }
+      if ((e = table_copy(c, c->d_hlg, hlg.data(), hlg.size() * sizeof(float4))) != hipSuccess)
+        return hip_fail(c, e, "HLG table upload");
+    }
   }
   c->params = *p;
   c->k = k;
@@ -999,7 +1029,10 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->rep_rs = k.expand_rep && k.shift_out ? 8 - k.shift_out : 31;
   F->dither = k.dither;
   F->out8 = p->bits_out == 8 ? 1 : 0;
-  F->pq_tab = c->d_pq;
+  // the table k_tile stages for its input transfer: the PQ EOTF, or for HLG
+  // input on the CPU chain the inverse OETF (the libplacebo branch keeps the
+  // PQ table for its IPT form and evaluates the HLG curve directly)
+  F->pq_tab = p->transfer_in == H2S_TRC_HLG && k.pipe != h2s::PIPE_LIBPLACEBO ? c->d_hlg : c->d_pq;
 }
 
 static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {

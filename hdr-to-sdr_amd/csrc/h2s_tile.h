@@ -122,7 +122,21 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
       const float hi = (fexp2((x - HLG_C) * (1.4426950408889634f / HLG_A)) + HLG_B) * (1.0f / 12.0f);
       return x <= 0.5f ? lo : hi;
     };
-    r = inv(er), g = inv(eg), b = inv(eb);
+    if (ESC == PQ_SEG) {
+      // the CPU chain's instances: the inverse OETF from the same LDS cubic
+      // table layout as the PQ EOTF (build_hlg_table; E staged as
+      // E*PQ_SEG + 1), the direct form past the table
+      r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
+      const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
+      constexpr float EI = 1.0f / (float)PQ_SEG;
+      if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {
+        r = er >= PQZ_LIM ? inv((er - 1.0f) * EI) : r;
+        g = eg >= PQZ_LIM ? inv((eg - 1.0f) * EI) : g;
+        b = eb >= PQZ_LIM ? inv((eb - 1.0f) * EI) : b;
+      }
+    } else {
+      r = inv(er), g = inv(eg), b = inv(eb);
+    }
     const float ys = 0.2627f * r + 0.6780f * g + 0.0593f * b;
     const float w = fexp2(flog2(ys) * 0.2f + F.log2_lin_scale);  // ys == 0 -> 0
     r *= w, g *= w, b *= w;
@@ -352,7 +366,9 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
                                              long long di, float& oyv, float& ozv, float qoff, float ydq) {
-  constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
+  // E in table-segment units for the table forms: the PQ EOTF, and the HLG
+  // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
+  constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
   const float eb = fmaf(U, K.a_bu, ybs);
@@ -694,12 +710,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
-  __shared__ float4 pq_lds[(TRC == 0 || LP) ? PQ_NSEG + 1 : 1];   // [0] = zero segment (pq_z)
+  __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
   __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
-  constexpr int ESC = TRC == 0 ? PQ_SEG : 1;
+  constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
 
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
@@ -714,7 +730,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
   const unsigned eq0 = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * t, 0, 0);  // out of range -> 0
   float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  const bool stage_pq = TRC == 0 || (LP && F.lp_ipt);   // block-uniform
+  const bool stage_pq = TRC == 0 || !LP || F.lp_ipt;   // block-uniform
   if (stage_pq && t < PQ_NSEG) {
     const __amdgpu_buffer_rsrc_t rpq = __builtin_amdgcn_make_buffer_rsrc((void*)F.pq_tab, (short)0, 16 * PQ_NSEG, 0x00020000);
     pq0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpq, 16 * t, 0, 0));
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   // hot constants live in VGPRs for the whole kernel.  Staged samples:
   // luma Y*ys + y_off (+1 on PQ: pq_z's zero segment), chroma centred on its
   // midpoint code (exact), so E = Y' + a*{U,V} takes 4 FMAs
-  const float yoff = in_vgpr(F.y_off_c) * (float)ESC + (TRC == 0 ? 1.0f : 0.0f);
+  const float yoff = in_vgpr(F.y_off_c) * (float)ESC + (ESC == PQ_SEG ? 1.0f : 0.0f);
   const float cmid = in_vgpr(F.c_mid);
   const float a_rv = in_vgpr(F.a_rv[1]) * (float)ESC, a_gv = in_vgpr(F.a_gv[1]) * (float)ESC,
               a_gu = in_vgpr(F.a_gu[1]) * (float)ESC, a_bu = in_vgpr(F.a_bu[1]) * (float)ESC;
