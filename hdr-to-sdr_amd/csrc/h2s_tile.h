@@ -473,7 +473,11 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
 constexpr int CBW = 32, CBH = 16;  // chroma tile
 constexpr int YST = 68;            // LDS row stride (floats) of the luma tile
 constexpr int HST = 68;            // LDS row stride of the horizontally upsampled chroma rows
-constexpr int NT = 2;              // buffer-op aux bits: non-temporal (streamed frame bytes)
+// buffer-op aux bits: non-temporal (streamed frame bytes).  Frame loads that
+// bypass the L1 (sc1 nt, sc0 sc1 nt) or use workgroup scope (sc0 nt) time the
+// same within 1 %: the streamed bytes do not evict the lattice lines the
+// gathers wait on (profiles/r03/ablations/frame_load_cache_policy.log)
+constexpr int NT = 2;
 
 __device__ __forceinline__ float quad_sum(float v) {
   // (v0 + v1) + (v2 + v3) over the 2x2 pixels of a quad, in all 4 lanes
