@@ -45,6 +45,9 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
   if (nt == 0) return hipSuccess;
   const long long nb = (nt + F.tpb - 1) / F.tpb;
   dim3 grid((unsigned)nb);
+  // (5 blocks per CU, the LDS bound; 4 and 3, forced by padding this
+  // allocation, measured +4 % and +42 % on the bench content:
+  // profiles/r03/ablations/blocks_per_cu.log)
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8 || lp) desat = 0;
   switch (dbg) {
