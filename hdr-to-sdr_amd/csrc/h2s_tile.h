@@ -709,7 +709,9 @@ __device__ __forceinline__ void put_chroma(const FastParams& F, const TileGeo& g
 // path on plain R'G'B' records (truncating output), BT.709 Y'CbCr at depth q
 template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 // 5 waves per SIMD = the LDS-bound occupancy (5 blocks of ~27.6 KB per CU;
-// 3 and 6 measured slower): let the compiler use the VGPRs that allows
+// 3, 4 and 6 measured slower on the bench content, 6 by 4.5 % in round 3 at
+// 80 VGPRs: profiles/r03/ablations/six_waves.log, blocks_per_cu.log): let
+// the compiler use the VGPRs that allows
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
