@@ -482,7 +482,10 @@ constexpr int NT = 2;
 __device__ __forceinline__ float quad_sum(float v) {
   // (v0 + v1) + (v2 + v3) over the 2x2 pixels of a quad, in all 4 lanes
   // (quad_perm [1,0,3,2] pairs horizontally, then [2,3,0,1] adds the rows):
-  // the oracle's summation order, so the chroma sum is bit-identical
+  // the oracle's summation order, so the chroma sum is bit-identical.  (The
+  // lane moves as ds_swizzle through the LDS crossbar with full-rate adds:
+  // 2-3 % slower, the swizzle latency sits in every step's chain;
+  // profiles/r03/ablations/quad_sum_swizzle_*.log)
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
   return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
 }
