@@ -977,6 +977,19 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
     F->a_bu[odd] = (float)(mbcb * cs / d);
   }
   F->log2_lin_scale = (float)log2((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl);
+  {
+    // k_tile takes a tile's steps without the exact-path ballot when every
+    // pixel's E stays below the table's end: staged luma <= safe_y and
+    // |centred chroma| <= safe_c (the legal half-range) give
+    // E <= Y' + max_c sum |a| * safe_c < PQ_EMAX.  Table forms only (E staged
+    // in segment units + 1); the direct HLG form has no exact path
+    const bool table = p->transfer_in == H2S_TRC_PQ || k.pipe != h2s::PIPE_LIBPLACEBO;
+    const double safe_c = (double)(112 << sh);
+    const double amax = std::max(std::max(fabs(mrcr), fabs(mgcb) + fabs(mgcr)), fabs(mbcb)) * cs;
+    const double ymax = (double)h2s::PQ_EMAX - amax * safe_c - 1e-3;
+    F->safe_c = table ? (float)safe_c : HUGE_VALF;
+    F->safe_y = table ? (float)(ymax * h2s::PQ_SEG + 1.0) : HUGE_VALF;
+  }
   F->lr = k.lr, F->lg = k.lg, F->lb = k.lb, F->desat = k.desat;
   F->rein_p = k.rein_p, F->rein_k = k.rein_k;
   F->hable_peak_inv = k.hable_peak_inv;

@@ -183,6 +183,9 @@ struct FastParams : CurveConsts {
   float2* chr444;
   int chr_w;
   float inv_c56;
+  // k_tile's branch-free tiles: every staged luma <= safe_y and every centred
+  // chroma code <= safe_c bound E below the EOTF table's end (resolve_fast)
+  float safe_y, safe_c;
   // S1 PQ EOTF (x 10000/npl) as a piecewise cubic: segment i covers
   // E in [i, i+1)/PQ_SEG, coefficients (c3, c2, c1, c0) of t = E*PQ_SEG - i
   const float4* pq_tab;

@@ -6,12 +6,18 @@
 
 namespace h2s {
 
-H2S_TILE_INSTANCE(0)
-H2S_TILE_EXTERN(1)
-H2S_TILE_EXTERN(2)
-H2S_TILE_EXTERN(3)
-H2S_TILE_EXTERN(4)
-H2S_TILE_EXTERN(5)
+H2S_TILE_INSTANCE(0, 0)
+H2S_TILE_EXTERN(0, 1)   // h2s_fast_lp.hip
+H2S_TILE_EXTERN(1, 0)
+H2S_TILE_EXTERN(1, 1)
+H2S_TILE_EXTERN(2, 0)
+H2S_TILE_EXTERN(2, 1)
+H2S_TILE_EXTERN(3, 0)
+H2S_TILE_EXTERN(3, 1)
+H2S_TILE_EXTERN(4, 0)
+H2S_TILE_EXTERN(4, 1)
+H2S_TILE_EXTERN(5, 0)
+H2S_TILE_EXTERN(5, 1)
 
 // YUV-premultiplied lattice (12-byte records, .cube order):
 // ((16 + 219*Y)*s + 0.5, 224*s*Cb/4, 224*s*Cr/4) with Y, Cb, Cr the BT.709
@@ -50,14 +56,17 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
   // profiles/r03/ablations/blocks_per_cu.log)
   const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8 || lp) desat = 0;
+#define H2S_DISPATCH(D) \
+  return lp ? launch_tile<D, 1>(F, trc, tm, desat, grid, lds, s) : launch_tile<D, 0>(F, trc, tm, desat, grid, lds, s)
   switch (dbg) {
-    case 0: return launch_tile<0>(F, trc, tm, desat, lp, grid, lds, s);
-    case 1: return launch_tile<1>(F, trc, tm, desat, lp, grid, lds, s);
-    case 2: return launch_tile<2>(F, trc, tm, desat, lp, grid, lds, s);
-    case 3: return launch_tile<3>(F, trc, tm, desat, lp, grid, lds, s);
-    case 4: return launch_tile<4>(F, trc, tm, desat, lp, grid, lds, s);
-    default: return launch_tile<5>(F, trc, tm, desat, lp, grid, lds, s);
+    case 0: H2S_DISPATCH(0);
+    case 1: H2S_DISPATCH(1);
+    case 2: H2S_DISPATCH(2);
+    case 3: H2S_DISPATCH(3);
+    case 4: H2S_DISPATCH(4);
+    default: H2S_DISPATCH(5);
   }
+#undef H2S_DISPATCH
 }
 
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st) {

@@ -6,7 +6,9 @@
 
 namespace h2s {
 
-H2S_TILE_INSTANCE(1)
-H2S_TILE_INSTANCE(2)
+H2S_TILE_INSTANCE(1, 0)
+H2S_TILE_INSTANCE(1, 1)
+H2S_TILE_INSTANCE(2, 0)
+H2S_TILE_INSTANCE(2, 1)
 
 }  // namespace h2s

@@ -6,8 +6,11 @@
 
 namespace h2s {
 
-H2S_TILE_INSTANCE(3)
-H2S_TILE_INSTANCE(4)
-H2S_TILE_INSTANCE(5)
+H2S_TILE_INSTANCE(3, 0)
+H2S_TILE_INSTANCE(3, 1)
+H2S_TILE_INSTANCE(4, 0)
+H2S_TILE_INSTANCE(4, 1)
+H2S_TILE_INSTANCE(5, 0)
+H2S_TILE_INSTANCE(5, 1)
 
 }  // namespace h2s

@@ -27,6 +27,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "h2s_device.h"
 
 namespace h2s {
@@ -98,13 +100,16 @@ __device__ __forceinline__ float pqi(const float4* tab, float y) {
 // returns true (wave-uniform) when some lane of the wave took the exact PQ
 // path: linear values may then be huge or infinite, and the tone curve must
 // use its overflow-safe form
-template <int TRC, int ESC = 1>
+// NOEX: the caller knows no E reaches the table's end (a tile of legal codes,
+// see k_tile): no ballot, no exact path, so a step has no branch
+template <int TRC, int ESC = 1, bool NOEX = false>
 __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
                                           float& r, float& g, float& b) {
   if (TRC == 0) {
     // E arrives as E*PQ_SEG + 1 (pq_z)
     static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
     r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
+    if (NOEX) return false;
     const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
     constexpr float EI = 1.0f / (float)PQ_SEG;
     if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {  // rare: extreme out-of-gamut codes
@@ -129,7 +134,7 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
       r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
       const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
       constexpr float EI = 1.0f / (float)PQ_SEG;
-      if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {
+      if (!NOEX && __builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {
         r = er >= PQZ_LIM ? inv((er - 1.0f) * EI) : r;
         g = eg >= PQZ_LIM ? inv((eg - 1.0f) * EI) : g;
         b = eb >= PQZ_LIM ? inv((eb - 1.0f) * EI) : b;
@@ -361,7 +366,7 @@ struct StepK {
 // the output depth (returned) and the pixel's two chroma quantiser
 // contributions (oyv, ozv) for the 2x2 sum.  di: this pixel's index in the
 // debug planes (DBG > 0, frame 0), else -1.
-template <int TRC, int TM, int DESAT, int LP, int DBG>
+template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
@@ -373,7 +378,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
   const float eb = fmaf(U, K.a_bu, ybs);
   float r, gg, bl;
-  const bool safe = to_linear<TRC, ESC>(F, pq_lds, er, eg, eb, r, gg, bl);
+  const bool safe = to_linear<TRC, ESC, NOEX>(F, pq_lds, er, eg, eb, r, gg, bl);
   const long long dpl = (long long)F.dbg_w * F.H;
   auto dput = [&](float a, float b_, float c) {
     if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
@@ -616,27 +621,37 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 
 // staging and store helpers of k_tile
 // 8 luma samples -> Y*ys + y_off floats at (row, 8 col8)
-__device__ __forceinline__ void stage_luma(float* yin, uint4 a, int row, int col8, float ysc, float yoff) {
+// returns the largest staged value
+__device__ __forceinline__ float stage_luma(float* yin, uint4 a, int row, int col8, float ysc, float yoff) {
   float v[8];
   unpack8(a, v);
   float* d = yin + row * YST + 8 * col8;
-  *reinterpret_cast<float4*>(d) = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
-  *reinterpret_cast<float4*>(d + 4) = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
+  const float4 lo = make_float4(fmaf(v[0], ysc, yoff), fmaf(v[1], ysc, yoff), fmaf(v[2], ysc, yoff), fmaf(v[3], ysc, yoff));
+  const float4 hi = make_float4(fmaf(v[4], ysc, yoff), fmaf(v[5], ysc, yoff), fmaf(v[6], ysc, yoff), fmaf(v[7], ysc, yoff));
+  *reinterpret_cast<float4*>(d) = lo;
+  *reinterpret_cast<float4*>(d + 4) = hi;
+  return __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(lo.x, lo.y), __builtin_fmaxf(lo.z, lo.w)),
+                         __builtin_fmaxf(__builtin_fmaxf(hi.x, hi.y), __builtin_fmaxf(hi.z, hi.w)));
 }
 // horizontal pass (left siting, x2 scale) on centred codes c = code - mid:
 // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float.  tt: chunk index
 // (row tt >> 2, 8-sample chunk tt & 3) of the tile's 18 x 4 chroma chunks
-__device__ __forceinline__ void stage_chroma(float* plane, uint4 a, unsigned h, int tt, float cmid) {
+// returns the largest |centred code|
+__device__ __forceinline__ float stage_chroma(float* plane, uint4 a, unsigned h, int tt, float cmid) {
   float v[9];
   unpack8(a, v);
   v[8] = (float)h;
 #pragma unroll
   for (int k = 0; k < 9; k++) v[k] -= cmid;
+  float m = fabsf(v[0]);
+#pragma unroll
+  for (int k = 1; k < 9; k++) m = __builtin_fmaxf(m, fabsf(v[k]));
   float* d = plane + (tt >> 2) * HST + 16 * (tt & 3);
 #pragma unroll
   for (int k = 0; k < 4; k++)
     *reinterpret_cast<float4*>(d + 4 * k) =
         make_float4(v[2 * k] + v[2 * k], v[2 * k] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 1], v[2 * k + 1] + v[2 * k + 2]);
+  return m;
 }
 // luma codes of tile row r, chunk c (8 pixels), packed for one 16-byte (u16)
 // / 8-byte (u8: .xy) store
@@ -722,6 +737,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
   __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
+  __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -753,6 +769,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   }
   if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (t < 2) tflag[t] = 0;
+  __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
     const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
     for (int i = t; i < PQI_NSEG; i += 256)
@@ -796,8 +814,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   // multiples of 8), so its luma offset is one constant
   const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
 
-  // the 8 compute steps of one tile (compute waves)
-  auto steps = [&](const TileGeo& g) {
+  // the 8 compute steps of one tile; FB (fast body): no pixel of the tile can
+  // reach the exact EOTF path and there is no BICUBIC scratch, so the 8 steps
+  // are one straight-line block the scheduler can interleave
+  auto steps = [&](const TileGeo& g, auto fast) {
+    constexpr bool FB = decltype(fast)::value;
     // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
     // frame, read through the scalar cache; the frame index is block-uniform)
     CurveConsts cv = F;
@@ -816,9 +837,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                                : -1;
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
-      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG>(
+      reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
           F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
-      if (F.chr444) {
+      if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
         // (the scratch has whole tiles of rows: rows past F.H are written, never read)
@@ -844,8 +865,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       mask_in(cur.ya), mask_in(cur.ua);
       cur.uh &= F.in_mask2;
     }
-    stage_luma(yin, cur.ya, t >> 3, t & 7, ysc, yoff);
-    if ((t & 127) < 72) stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
+    const float my = stage_luma(yin, cur.ya, t >> 3, t & 7, ysc, yoff);
+    float mc = 0.0f;
+    if ((t & 127) < 72) mc = stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
+    const int par = (int)(tile & 1u);
+    if ((my > F.safe_y || mc > F.safe_c)) tflag[par] = 1;
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
@@ -853,7 +877,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
       cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
     __syncthreads();
-    steps(g);
+    const bool fb = __builtin_amdgcn_readfirstlane(tflag[par]) == 0 && !F.chr444;
+    if (t == 0) tflag[par ^ 1] = 0;   // for the next tile: read by every wave of the previous one before this barrier
+    if (fb)
+      steps(g, std::integral_constant<bool, true>{});
+    else
+      steps(g, std::integral_constant<bool, false>{});
     __syncthreads();
 
     // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
@@ -901,22 +930,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   X(1, 6, 0, 1)
 
 // one DBG value's instances (0 = product kernels; 1..5 = the debug instance
-// for that h2s_stage), explicitly instantiated in exactly one .hip each
-template <int DBG>
-hipError_t launch_tile(const FastParams& F, int trc, int tm, int desat, int lp, dim3 grid, size_t lds,
-                       hipStream_t s) {
-#define X(T, M, D, L)                                                                     \
-  if (trc == T && tm == M && desat == D && lp == L) {                                     \
-    hipLaunchKernelGGL((k_tile<T, M, D, L, DBG>), grid, dim3(256), lds, s, F);            \
-    return hipGetLastError();                                                             \
+// for that h2s_stage) of one chain (LPI 0: the CPU chain, 1: the libplacebo
+// branch), explicitly instantiated in exactly one .hip each: the two chains'
+// product instances compile in their own translation units, so each gets the
+// scheduler that measured fastest for it (_build.py SOURCE_FLAGS)
+template <int DBG, int LPI>
+hipError_t launch_tile(const FastParams& F, int trc, int tm, int desat, dim3 grid, size_t lds, hipStream_t s) {
+#define X(T, M, D, L)                                                                       \
+  if constexpr (L == LPI) {                                                                 \
+    if (trc == T && tm == M && desat == D) {                                                \
+      hipLaunchKernelGGL((k_tile<T, M, D, L, DBG>), grid, dim3(256), lds, s, F);            \
+      return hipGetLastError();                                                             \
+    }                                                                                       \
   }
   FAST_CASES(X)
 #undef X
   return hipErrorInvalidValue;
 }
-#define H2S_TILE_EXTERN(D) \
-  extern template hipError_t launch_tile<D>(const FastParams&, int, int, int, int, dim3, size_t, hipStream_t);
-#define H2S_TILE_INSTANCE(D) \
-  template hipError_t launch_tile<D>(const FastParams&, int, int, int, int, dim3, size_t, hipStream_t);
+#define H2S_TILE_EXTERN(D, L) \
+  extern template hipError_t launch_tile<D, L>(const FastParams&, int, int, int, dim3, size_t, hipStream_t);
+#define H2S_TILE_INSTANCE(D, L) \
+  template hipError_t launch_tile<D, L>(const FastParams&, int, int, int, dim3, size_t, hipStream_t);
 
 }  // namespace h2s
