@@ -730,7 +730,10 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 // 3, 4 and 6 measured slower on the bench content, 6 by 4.5 % in round 3 at
 // 80 VGPRs: profiles/r03/ablations/six_waves.log, blocks_per_cu.log): let
 // the compiler use the VGPRs that allows
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_tile(const FastParams F) {
+#ifndef H2S_TILE_WPE
+#define H2S_TILE_WPE 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WPE))) void k_tile(const FastParams F) {
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions

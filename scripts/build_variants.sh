@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build libh2s variants for scripts/time_variants.py.
 # Usage: bash scripts/build_variants.sh NAME:"-DFLAG ..." NAME2:"..."
-# Only the product tile instances (h2s_fast.hip) are rebuilt with the flags;
+# Only the product tile instances (h2s_fast.hip, h2s_fast_lp.hip) are rebuilt
+# with the flags;
 # every other object comes from the in-tree build (hdr-to-sdr_amd/build/obj,
 # run `python -c "import __graft_entry__ as g; g.build()"` first).
 # Outputs scripts/variants/libh2s_NAME.so (git-ignored, travels with gpurun).
@@ -11,16 +12,18 @@ C=$ROOT/hdr-to-sdr_amd/csrc
 O=$ROOT/hdr-to-sdr_amd/build/obj
 V=$ROOT/scripts/variants
 mkdir -p "$V"
-FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed -mllvm -amdgpu-sched-strategy=max-memory-clause"
+FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed"
+MMC="-mllvm -amdgpu-sched-strategy=max-memory-clause"   # _build.py SOURCE_FLAGS (h2s_fast.hip only)
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   [ "$flags" = "$spec" ] && flags=""
   (
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fast_$name.o" "$C/h2s_fast.hip" &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $MMC $flags -c -o "$V/fast_$name.o" "$C/h2s_fast.hip" &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fastlp_$name.o" "$C/h2s_fast_lp.hip" &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" "$V/fastlp_$name.o" \
       "$O/h2s_fast_dbg345.hip.o" "$O/h2s_fast_dbg12.hip.o" "$O/h2s_api.hip.o" "$O/h2s_kernels.hip.o" \
-      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o"
+      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o" "$V/fastlp_$name.o"
   ) &
   pids+=($!)
 done
