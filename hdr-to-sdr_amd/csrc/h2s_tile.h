@@ -447,8 +447,10 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
     // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
-    // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL)
-    o.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, ydq))));
+    // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL);
+    // on the libplacebo branch o.x is lut3d's R, and the dither belongs to
+    // the luma quantiser below
+    o.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, LP ? 0.0f : ydq))));
     if (LP) {
       // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
       // Y'CbCr at depth q in the generic kernel's operation order; o = (luma

@@ -162,6 +162,10 @@ LP_CASES = {
     'bt2390_pq12_p010_truncate': dict(tonemapper='bt.2390', bits_in=12, bits_out=10, lp_p010='truncate'),
     'lp_hable_hlg12_p010_truncate_dither': dict(tonemapper='hable', pipeline='libplacebo', bits_in=12, bits_out=12,
                                                transfer='arib-std-b67', lp_p010='truncate', lp_dither='ordered'),
+    # the S6 swscale dither (App. B.4) after the branch's eq / 8-bit output:
+    # it acts on the final luma quantiser only, never on lut3d's input
+    'bt2390_gamma13_eq_sws_dither': dict(tonemapper='bt.2390', gamma=1.3, dither='ordered'),
+    'bt2390_8bit_sws_dither': dict(tonemapper='bt.2390', bits_out=8, dither='ordered'),
 }
 
 
@@ -180,7 +184,8 @@ def test_libplacebo_branch_matches_oracle(tm, case, kind):
 @pytest.mark.parametrize('case', ['C3_bt2390', 'spline', 'bt2390_gamma13_eq', 'bt2390_hlg12', 'bt2390_max_rgb',
                                   'bt2390_lut_off_nv12', 'bt2390_max_rgb_lut_off', 'lp_hable', 'lp_mobius_max_rgb',
                                   'lp_reinhard_hlg12_lut_off', 'bt2390_range_limited', 'bt2390_dither_ordered',
-                                  'bt2390_pq12_p010_truncate', 'lp_hable_hlg12_p010_truncate_dither'])
+                                  'bt2390_pq12_p010_truncate', 'lp_hable_hlg12_p010_truncate_dither',
+                                  'bt2390_gamma13_eq_sws_dither', 'bt2390_8bit_sws_dither'])
 def test_libplacebo_tile_equals_generic(tm, case):
     """The two kernels of the libplacebo branch against each other (same
     device, same float32 formulas up to the tile kernel's PQ table): the
