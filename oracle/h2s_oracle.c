@@ -429,6 +429,15 @@ static float sanitizef(float f) {
 
 static float clipf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+/* the S6 input clip to [0, 1] with NaN taken as 0.  vf_tonemap's float32
+ * desaturation turns codes far past the EOTF's range into NaN (inf - inf).
+ * On the LUT path lut3d's sanitizef maps such a channel to 0; with the LUT
+ * off the value reaches swscale's float -> int conversion, whose result for
+ * NaN is not defined (x86 lrintf: INT_MIN).  The channel is taken as 0 there
+ * too, per channel, so one NaN does not blank the whole Y'CbCr sample
+ * (PARITY UNPINNED: no ffmpeg here to settle it). */
+static float clip01n(float v) { return v > 0.0f ? (v < 1.0f ? v : 1.0f) : 0.0f; }
+
 /* lattice point (ri, gi, bi) in .cube order (red fastest). */
 static rgbf lat(const ocfg *c, int ri, int gi, int bi) {
   const float *e = c->lut + 3 * (((size_t)bi * c->lut_n + gi) * c->lut_n + ri);
@@ -619,9 +628,9 @@ static rgbf chain_px(const ocfg *c, float y, float cb, float cr, int upto, int p
   m.r = M2020_709[0][0] * t.r + M2020_709[0][1] * t.g + M2020_709[0][2] * t.b;
   m.g = M2020_709[1][0] * t.r + M2020_709[1][1] * t.g + M2020_709[1][2] * t.b;
   m.b = M2020_709[2][0] * t.r + M2020_709[2][1] * t.g + M2020_709[2][2] * t.b;
-  g.r = clipf(bt1886_inverse(m.r), 0.0f, 1.0f);
-  g.g = clipf(bt1886_inverse(m.g), 0.0f, 1.0f);
-  g.b = clipf(bt1886_inverse(m.b), 0.0f, 1.0f);
+  g.r = clip01n(bt1886_inverse(m.r));
+  g.g = clip01n(bt1886_inverse(m.g));
+  g.b = clip01n(bt1886_inverse(m.b));
   return g;
 }
 
@@ -887,7 +896,7 @@ static yuvf px_yuv(const ocfg *c, const h2s_frames *in, int f, int x, int y) {
   float cb = upsample(c, in, 1, f, x, y, cw, ch);
   float cr = upsample(c, in, 2, f, x, y, cw, ch);
   rgbf o = chain_px(c, yv, cb, cr, 99, x, y);
-  float R = clipf(o.r, 0.0f, 1.0f), G = clipf(o.g, 0.0f, 1.0f), B = clipf(o.b, 0.0f, 1.0f);
+  float R = clip01n(o.r), G = clip01n(o.g), B = clip01n(o.b);
   float Y = K709_R * R + K709_G * G + K709_B * B;
   yuvf r = {(16.0f + 219.0f * Y) * s, cbr * R + cbg * G + cbb * B, crr * R + crg * G + crb * B};
   return r;
