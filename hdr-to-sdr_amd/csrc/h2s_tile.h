@@ -440,17 +440,35 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
     const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
     const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
-    const f3 c0 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0);
-    const f3 c1 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0);
-    const f3 c2 = __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0);
-    const f3 c3 = __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0);
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
-    o = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
-    // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
-    // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL);
-    // on the libplacebo branch o.x is lut3d's R, and the dither belongs to
-    // the luma quantiser below
-    o.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, LP ? 0.0f : ydq))));
+    auto blend = [&](const f3 c0, const f3 c1, const f3 c2, const f3 c3) {
+      f3 r = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
+      // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
+      // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL);
+      // on the libplacebo branch o.x is lut3d's R, and the dither belongs to
+      // the luma quantiser below
+      r.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, LP ? 0.0f : ydq))));
+      return r;
+    };
+    // CPU chain: when every lane of the step is in one cell and one
+    // tetrahedron, its four records come through the scalar cache and the
+    // step issues no vector-memory gather (bit-identical; C2 -1.8 % smooth,
+    // -5 % on the website frame; the libplacebo instances measured +8 %,
+    // SGPR-bound, and keep the gathers: profiles/r03/ablations/sgather_*.log)
+    const int b0 = __builtin_amdgcn_readfirstlane(base), m0 = __builtin_amdgcn_readfirstlane(om),
+              n0 = __builtin_amdgcn_readfirstlane(ocn);
+    if (!LP && __builtin_amdgcn_ballot_w64(base != b0 || om != m0 || ocn != n0) == 0) {
+      typedef __attribute__((address_space(4))) const float cfl;
+      cfl* L = (cfl*)F.lut_yuv;
+      auto sl = [&](int off) {
+        const int i = off >> 2;
+        return f3{L[i], L[i + 1], L[i + 2]};
+      };
+      o = blend(sl(b0), sl(b0 + m0), sl(b0 + n0), sl(b0 + F.c111));
+    } else
+    o = blend(__builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0), __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0),
+              __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0),
+              __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0));
     if (LP) {
       // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
       // Y'CbCr at depth q in the generic kernel's operation order; o = (luma

@@ -19,8 +19,13 @@ tm_name = os.environ.get('TM', 'hable')
 p = hdr2sdr.TonemapParams(tonemapper=tm_name, gamma=2.2, bits_in=10, bits_out=10, mode='compat8')
 tm = hdr2sdr.Tonemapper(0, p, hdr2sdr.generate_lattice(65))
 res = {}
-for kind in ('smooth', 'uniform', 'edges'):
-    src = synth_frames(kind, 16, 3840, 2160, 10, device=dev, seed=0x5EED)
+for kind in os.environ.get('KINDS', 'smooth,uniform,edges').split(','):
+    if kind == 'website':   # the reference's own 4K HDR frame, 16 copies (as bench.py's real_content line)
+        from hdr2sdr.synth import frames_from_rgb8
+        z = np.load(os.path.join(REPO, 'tests', 'golden', 'website_hdr_full.npz'))
+        src = frames_from_rgb8(z[z.files[0]], 16, 10, dev)
+    else:
+        src = synth_frames(kind, 16, 3840, 2160, 10, device=dev, seed=0x5EED)
     dst = hdr2sdr.FrameBatch.empty_torch(16, 3840, 2160, 10, dev)
     s = torch.cuda.current_stream(dev)
     for _ in range(3): tm.process(src, dst, s)
