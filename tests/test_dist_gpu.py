@@ -102,3 +102,41 @@ def test_two_ranks_on_libh2s_equal_one_process(tmp_path, case):
     for r in res:
         assert int(r[0]) == n * w * h       # SUM of pixels over ranks
         assert int(r[1]) == cks             # SUM of shard checksums == the one-process checksum
+
+
+_RCCL_CHILD = r'''
+import os, sys
+sys.path[:0] = [os.path.join(REPO, 'hdr-to-sdr_amd'), REPO]
+import numpy as np, torch, torch.distributed as dist
+import hdr2sdr
+from hdr2sdr.dist import broadcast_setup, reduce_run, gather_peak_stats
+dev = torch.device('cuda', 0)
+torch.cuda.set_device(dev)
+dist.init_process_group('nccl', device_id=dev)
+assert dist.get_backend() == 'nccl'
+p = hdr2sdr.TonemapParams(tonemapper='mobius', gamma=1.0, bits_out=10)
+lat = hdr2sdr.generate_lattice(17)
+p2, lat2 = broadcast_setup(p, lat, 17, dev)
+assert p2 == p and np.array_equal(lat2, lat)
+px, cks, el = reduce_run(123, 456, 0.25, dev)
+assert (px, cks, el) == (123, 456, 0.25)
+st = gather_peak_stats(np.array([1.0, 2.0]), np.array([0.5, 0.25]), 2, dev)
+assert np.array_equal(st, [[1.0, 0.5], [2.0, 0.25]])
+dist.barrier()
+dist.destroy_process_group()
+print('RCCL OK')
+'''
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_world1():
+    """The nccl (= RCCL) backend through hdr2sdr/dist.py's collectives with
+    device tensors (bench.py's N > 1 path: params + lattice broadcast, the
+    SUM / MAX reduction, the peak-statistics all-gather) in a world of one
+    rank on the box's one card; only the driver's 8-GPU run has more ranks."""
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), RANK='0', WORLD_SIZE='1',
+               LOCAL_RANK='0')
+    r = subprocess.run([sys.executable, '-c', 'REPO=%r\n' % REPO + _RCCL_CHILD], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and 'RCCL OK' in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
