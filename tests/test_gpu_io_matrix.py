@@ -25,6 +25,11 @@ CASES = {
     'cpu_hlg12_replicate_dither': dict(tonemapper='hable', transfer='arib-std-b67', bits_in=12, bits_out=12,
                                        expand='replicate', dither='ordered'),
     'lp_spline_8bit_bicubic': dict(tonemapper='spline', bits_out=8, chroma_filter='bicubic'),
+    # dynamic peak with the per-frame two-pass chroma, and with both dithers
+    'lp_bt2390_peak_detect_bicubic': dict(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0,
+                                          chroma_filter='bicubic'),
+    'lp_spline_peak_detect_dithers_eq': dict(tonemapper='spline', peak_detect=True, maxcll=4000.0, gamma=1.3,
+                                             dither='ordered', lp_dither='ordered'),
 }
 F, W, H = 7, 200, 70   # uneven chunks; 3 whole tiles + an 8-pixel generic tail per row; 16-byte rows
 
