@@ -135,6 +135,26 @@ def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline, mo
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('kw', [dict(chroma_filter='bicubic'), dict(gamma=1.3, dither='ordered', lp_dither='ordered'),
+                                dict(lp_range='limited', bits_out=8)])
+def test_gpu_dynamic_peak_with_switches_matches_oracle(kw):
+    """Dynamic peak (per-frame curve records) together with the two-pass
+    BICUBIC chroma (one launch pair per frame), the two dithers with eq, and
+    range=tv at an 8-bit output, against the oracle's sequential flow."""
+    from test_gpu_parity import assert_close_int, lattice
+    W, H = 200, 96
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0, **kw)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)
+    dst = hdr2sdr.FrameBatch.empty_numpy(buf.shape[0], W, H, params.bits_out)
+    tm.process(src, dst)
+    tm.close()
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
+
+
+@pytest.mark.gpu
 def test_gpu_peak_reset_restarts_the_sequence():
     from test_gpu_parity import lattice
     buf = sequence()
