@@ -13,7 +13,7 @@ from collections import defaultdict
 
 d = sys.argv[1]
 # the C2 instance k_tile<PQ, Hable, RGB desat, CPU chain, DBG 0>
-KERNEL = 'k_tile<0, 5, 2, 0, 0>'
+KERNEL = os.environ.get('H2S_PROF_KERNEL', 'k_tile<0, 5, 2, 0, 0>')   # (H2S_PROF_KERNEL: another instance)
 
 for f in glob.glob(os.path.join(d, 'trace', '**', '*kernel_stats.csv'), recursive=True):
     print('## kernel stats', os.path.relpath(f, d))
