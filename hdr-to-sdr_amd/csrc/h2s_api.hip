@@ -21,11 +21,12 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
 hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s);
 hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
-hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
-                            long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
-                            hipStream_t s);
+hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, long long sfp, uint8_t* dst, int ow,
+                            int oh, long long dls, long long dfp, const float* wx, const int* sx, const float* wy,
+                            const int* sy, int T, int nframes, hipStream_t s);
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
-                             int w, int h, uint8_t* rgb, long long rls, const uint8_t* glut, hipStream_t s);
+                             long long yuv_fp, int w, int h, uint8_t* rgb, long long rls, long long rgb_fp,
+                             const uint8_t* glut, int nframes, hipStream_t s);
 constexpr int PEAK_BLOCKS = 64;  // partial (max, sum) records per frame
 constexpr int PEAK_BINS = 1024;  // percentile histogram bins over PQ [0, 1] (h2s_kernels.hip)
 hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s);
@@ -708,7 +709,7 @@ void h2s_params_default(h2s_params* p) {
   p->lp_tone = H2S_LP_TONE_IPT;   // libplacebo >= 6 tone-maps in IPT (h2s.h enum h2s_lp_tone)
   p->lp_range = H2S_LP_RANGE_FULL;
   p->lp_dither = H2S_LP_DITHER_NONE;
-  p->lp_p010 = H2S_LP_P010_KEEP;
+  p->lp_p010 = H2S_LP_P010_TRUNCATE;   // format=p010,hwupload (src/utils.py:431)
   p->pd_smoothing = p->pd_scene_low = p->pd_scene_high = p->pd_percentile = p->pd_min_peak = NAN;
 }
 
@@ -1788,10 +1789,13 @@ int resize_taps(int src, int dst, std::vector<float>* w, std::vector<int>* start
 }
 }  // namespace
 
-int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rgb_linesize, int out_w, int out_h,
-                      double display_gamma, int rgb_location, void* hip_stream) {
+int h2s_preview_rgb24_batch(h2s_ctx* c, const h2s_frames* in, int nframes, uint8_t* rgb, int64_t rgb_linesize,
+                            int64_t rgb_frame_pitch, int out_w, int out_h, double display_gamma, int rgb_location,
+                            void* hip_stream) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
-  if (!rgb || out_w <= 0 || out_h <= 0 || rgb_linesize < 3LL * out_w)
+  if (nframes < 1) return fail(c, H2S_E_INVALID_ARG, "nframes must be >= 1");
+  if (!rgb || out_w <= 0 || out_h <= 0 || rgb_linesize < 3LL * out_w ||
+      (nframes > 1 && rgb_frame_pitch < rgb_linesize * out_h))
     return fail(c, H2S_E_INVALID_ARG, "bad RGB output geometry");
   if (!(display_gamma > 0.0)) return fail(c, H2S_E_INVALID_ARG, "display gamma must be > 0");
   if (!c->params_set) return fail(c, H2S_E_INVALID_ARG, "h2s_set_params was not called");
@@ -1838,14 +1842,22 @@ int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rg
     glut[i] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
   }
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t yuv_b = al((size_t)W * H * 3 / 2), syuv_b = scale ? al((size_t)out_w * out_h + 2 * (size_t)ow2 * oh2) : 0;
+  const size_t n = (size_t)nframes;
+  const size_t yfp = (size_t)W * H * 3 / 2;                             // tight yuv420p frame
+  const size_t sfp = (size_t)out_w * out_h + 2 * (size_t)ow2 * oh2;    // one resized frame
+  const size_t yuv_b = al(yfp * n), syuv_b = scale ? al(sfp * n) : 0;
   const size_t tab_b = scale ? al((wx.size() + wy.size() + wcx.size() + wcy.size()) * 4) +
                                    al((sx.size() + sy.size() + scx.size() + scy.size()) * 4)
                              : 0;
-  const size_t rgb_b = rgb_location == H2S_LOC_HOST ? al((size_t)out_w * 3 * out_h) : 0;
+  const size_t rgb_b = rgb_location == H2S_LOC_HOST ? al((size_t)out_w * 3 * out_h * n) : 0;
   const size_t need = yuv_b + syuv_b + tab_b + rgb_b + 256;
   if (need > c->prev_bytes) {
-    if (c->d_prev) hipFree(c->d_prev);
+    if (c->d_prev) {
+      // a previous preview's kernels may still read the old scratch
+      drain_launches(c);
+      hipStreamSynchronize(s);
+      hipFree(c->d_prev);
+    }
     c->d_prev = nullptr;
     c->prev_bytes = 0;
     if (hipMalloc(&c->d_prev, need) != hipSuccess) {
@@ -1858,10 +1870,28 @@ int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rg
   h2s_frames y8{};
   y8.width = W, y8.height = H, y8.bits = 8, y8.location = H2S_LOC_DEVICE;
   y8 = tight(&y8, base);
-  if ((rc = h2s_process(c, in, &y8, 1, hip_stream))) return rc;
+  if (c->params.peak_detect) {
+    // libplacebo branch: the reference converts each preview frame in its own
+    // ffmpeg run (extract_frames_with_gpu_conversion_batch loops
+    // extract_frame_with_gpu_conversion, src/utils.py:803-824), so peak
+    // detection starts afresh on every frame: one launch per frame, state
+    // reset in between
+    for (int f = 0; f < nframes; f++) {
+      h2s_frames fi = *in, fo = y8;
+      for (int k = 0; k < 3; k++) {
+        fi.data[k] = (uint8_t*)in->data[k] + (long long)f * in->frame_pitch[k];
+        fo.data[k] = (uint8_t*)y8.data[k] + (long long)f * y8.frame_pitch[k];
+      }
+      h2s_peak_reset(c);
+      if ((rc = h2s_process(c, &fi, &fo, 1, hip_stream))) return rc;
+    }
+    h2s_peak_reset(c);
+  } else if ((rc = h2s_process(c, in, &y8, nframes, hip_stream))) {  // one launch for the batch
+    return rc;
+  }
   hipError_t e = hipSuccess;
   const uint8_t *yp = (const uint8_t*)y8.data[0], *up = (const uint8_t*)y8.data[1], *vp = (const uint8_t*)y8.data[2];
-  long long yls = W, cls = W / 2;
+  long long yls = W, cls = W / 2, fp = (long long)yfp;
   uint8_t* p = base + yuv_b;
   if (scale) {
     uint8_t* sy_ = p;
@@ -1885,23 +1915,37 @@ int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rg
                 {dscx, scx.data(), scx.size() * 4}, {dscy, scy.data(), scy.size() * 4}};
     for (auto& u : up_)
       if (e == hipSuccess) e = hipMemcpyAsync(u.d, u.h, u.b, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = h2s::launch_resize_u8(yp, W, H, W, sy_, out_w, out_h, out_w, dwx, dsx, dwy, dsy, T, s);
+    const long long sp = (long long)sfp;
     if (e == hipSuccess)
-      e = h2s::launch_resize_u8(up, W / 2, H / 2, W / 2, su_, ow2, oh2, ow2, dwcx, dscx, dwcy, dscy, Tc, s);
+      e = h2s::launch_resize_u8(yp, W, H, W, fp, sy_, out_w, out_h, out_w, sp, dwx, dsx, dwy, dsy, T, nframes, s);
     if (e == hipSuccess)
-      e = h2s::launch_resize_u8(vp, W / 2, H / 2, W / 2, sv_, ow2, oh2, ow2, dwcx, dscx, dwcy, dscy, Tc, s);
-    yp = sy_, up = su_, vp = sv_, yls = out_w, cls = ow2;
+      e = h2s::launch_resize_u8(up, W / 2, H / 2, W / 2, fp, su_, ow2, oh2, ow2, sp, dwcx, dscx, dwcy, dscy, Tc,
+                                nframes, s);
+    if (e == hipSuccess)
+      e = h2s::launch_resize_u8(vp, W / 2, H / 2, W / 2, fp, sv_, ow2, oh2, ow2, sp, dwcx, dscx, dwcy, dscy, Tc,
+                                nframes, s);
+    yp = sy_, up = su_, vp = sv_, yls = out_w, cls = ow2, fp = sp;
   }
   uint8_t* dglut = base + need - 256;
-  uint8_t* drgb = rgb_location == H2S_LOC_HOST ? base + yuv_b + syuv_b + tab_b : rgb;
-  const long long drls = rgb_location == H2S_LOC_HOST ? 3LL * out_w : rgb_linesize;
+  const bool host = rgb_location == H2S_LOC_HOST;
+  uint8_t* drgb = host ? base + yuv_b + syuv_b + tab_b : rgb;
+  const long long drls = host ? 3LL * out_w : rgb_linesize;
+  const long long drfp = host ? 3LL * out_w * out_h : rgb_frame_pitch;
   if (e == hipSuccess) e = hipMemcpyAsync(dglut, glut, 256, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = h2s::launch_yuv8_rgb24(yp, yls, up, vp, cls, out_w, out_h, drgb, drls, dglut, s);
-  if (e == hipSuccess && rgb_location == H2S_LOC_HOST)
-    e = hipMemcpy2DAsync(rgb, rgb_linesize, drgb, drls, 3 * (size_t)out_w, out_h, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess)
+    e = h2s::launch_yuv8_rgb24(yp, yls, up, vp, cls, fp, out_w, out_h, drgb, drls, drfp, dglut, nframes, s);
+  for (int f = 0; host && f < nframes && e == hipSuccess; f++)
+    e = hipMemcpy2DAsync(rgb + (long long)f * rgb_frame_pitch, rgb_linesize, drgb + f * drfp, drls, 3 * (size_t)out_w,
+                         out_h, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "preview");
   return 0;
+}
+
+int h2s_preview_rgb24(h2s_ctx* c, const h2s_frames* in, uint8_t* rgb, int64_t rgb_linesize, int out_w, int out_h,
+                      double display_gamma, int rgb_location, void* hip_stream) {
+  return h2s_preview_rgb24_batch(c, in, 1, rgb, rgb_linesize, rgb_linesize * (int64_t)out_h, out_w, out_h,
+                                 display_gamma, rgb_location, hip_stream);
 }
 
 int h2s_set_timing(h2s_ctx* c, int enabled) {

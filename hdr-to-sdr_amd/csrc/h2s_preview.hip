@@ -2,9 +2,10 @@
 // :719-765; src/preview.py:108-117): aspect-fit resize of the 8-bit yuv420p
 // the chain produced, Y'CbCr -> RGB24 and the GUI's display gamma.
 //
-// The preview is one frame at a time and latency-bound (a 4K frame is ~25 MB
-// of RGB out), so these kernels are plain one-thread-per-output-sample
-// gathers; the tone-map work before them runs through k_tile.
+// The preview is latency-bound (a 4K frame is ~25 MB of RGB out), so these
+// kernels are plain one-thread-per-output-sample gathers; blockIdx.z is the
+// frame of a batch (extract_frames_with_conversion_batch, src/utils.py:668-716:
+// N frames, one call); the tone-map work before them runs through k_tile.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -15,12 +16,14 @@ namespace h2s {
 // separable resize of one u8 plane, taps/weights precomputed on the host per
 // output column (wx: ow x T, start sx) and row (wy: oh x T, start sy); source
 // indices clamp at the edges (swscale's edge handling)
-__global__ void k_resize_u8(const uint8_t* __restrict__ src, int sw, int sh, long long sls,
-                            uint8_t* __restrict__ dst, int ow, int oh, long long dls,
+__global__ void k_resize_u8(const uint8_t* __restrict__ src, int sw, int sh, long long sls, long long sfp,
+                            uint8_t* __restrict__ dst, int ow, int oh, long long dls, long long dfp,
                             const float* __restrict__ wx, const int* __restrict__ sx,
                             const float* __restrict__ wy, const int* __restrict__ sy, int T) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= ow || y >= oh) return;
+  src += blockIdx.z * sfp;
+  dst += blockIdx.z * dfp;
   float acc = 0.0f;
   for (int j = 0; j < T; j++) {
     int r = sy[y] + j;
@@ -41,10 +44,13 @@ __global__ void k_resize_u8(const uint8_t* __restrict__ src, int sw, int sh, lon
 // yuv420p (BT.709, limited) -> RGB24 full range, chroma of pixel (x, y) from
 // sample (x/2, y/2); then the display-gamma LUT
 __global__ void k_yuv8_rgb24(const uint8_t* __restrict__ yp, long long yls, const uint8_t* __restrict__ up,
-                             const uint8_t* __restrict__ vp, long long cls, int w, int h,
-                             uint8_t* __restrict__ rgb, long long rls, const uint8_t* __restrict__ glut) {
+                             const uint8_t* __restrict__ vp, long long cls, long long yuv_fp, int w, int h,
+                             uint8_t* __restrict__ rgb, long long rls, long long rgb_fp,
+                             const uint8_t* __restrict__ glut) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= w || y >= h) return;
+  yp += blockIdx.z * yuv_fp, up += blockIdx.z * yuv_fp, vp += blockIdx.z * yuv_fp;
+  rgb += blockIdx.z * rgb_fp;
   const float Y = 1.16438356f * ((float)yp[y * yls + x] - 16.0f);
   const float U = (float)up[(y >> 1) * cls + (x >> 1)] - 128.0f;
   const float V = (float)vp[(y >> 1) * cls + (x >> 1)] - 128.0f;
@@ -57,18 +63,19 @@ __global__ void k_yuv8_rgb24(const uint8_t* __restrict__ yp, long long yls, cons
   }
 }
 
-hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, uint8_t* dst, int ow, int oh,
-                            long long dls, const float* wx, const int* sx, const float* wy, const int* sy, int T,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(k_resize_u8, dim3((ow + 255) / 256, oh), dim3(256), 0, s, src, sw, sh, sls, dst, ow, oh, dls,
-                     wx, sx, wy, sy, T);
+hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, long long sfp, uint8_t* dst, int ow,
+                            int oh, long long dls, long long dfp, const float* wx, const int* sx, const float* wy,
+                            const int* sy, int T, int nframes, hipStream_t s) {
+  hipLaunchKernelGGL(k_resize_u8, dim3((ow + 255) / 256, oh, nframes), dim3(256), 0, s, src, sw, sh, sls, sfp, dst, ow,
+                     oh, dls, dfp, wx, sx, wy, sy, T);
   return hipGetLastError();
 }
 
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
-                             int w, int h, uint8_t* rgb, long long rls, const uint8_t* glut, hipStream_t s) {
-  hipLaunchKernelGGL(k_yuv8_rgb24, dim3((w + 255) / 256, h), dim3(256), 0, s, yp, yls, up, vp, cls, w, h, rgb, rls,
-                     glut);
+                             long long yuv_fp, int w, int h, uint8_t* rgb, long long rls, long long rgb_fp,
+                             const uint8_t* glut, int nframes, hipStream_t s) {
+  hipLaunchKernelGGL(k_yuv8_rgb24, dim3((w + 255) / 256, h, nframes), dim3(256), 0, s, yp, yls, up, vp, cls, yuv_fp, w,
+                     h, rgb, rls, rgb_fp, glut);
   return hipGetLastError();
 }
 

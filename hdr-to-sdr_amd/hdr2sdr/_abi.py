@@ -47,7 +47,7 @@ EXPORTS = (
     'h2s_abi_version', 'h2s_create', 'h2s_destroy', 'h2s_last_error',
     'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
     'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
-    'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_peak_reset',
+    'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_preview_rgb24_batch', 'h2s_peak_reset',
     'h2s_peak_state', 'h2s_peak_stats', 'h2s_peak_feed', 'h2s_set_option', 'h2s_query_path',
 )
 
@@ -176,6 +176,9 @@ def lib() -> ctypes.CDLL:
         'h2s_preview_rgb24': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                              ctypes.c_void_p]),
+        'h2s_preview_rgb24_batch': (ctypes.c_int, [c_ctx, ctypes.POINTER(H2SFrames), ctypes.c_int, ctypes.c_void_p,
+                                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_double, ctypes.c_int, ctypes.c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

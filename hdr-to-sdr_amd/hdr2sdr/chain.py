@@ -21,7 +21,7 @@ from __future__ import annotations
 import math
 import re
 from dataclasses import dataclass, replace
-from typing import Any
+from typing import Any, Callable
 
 from . import _abi
 
@@ -75,6 +75,39 @@ def is_gpu_only_tonemapper(tonemapper: str) -> bool:
     return tonemapper.lower() in GPU_ONLY_TONEMAPPERS
 
 
+# src/ffmpeg_command.py:241-245 (the message _filter_args raises)
+CPU_GPU_ONLY_ERROR = ("{tonemapper} requires GPU tonemapping; this item's settings force CPU processing "
+                      "— change the tonemapper or output bit depth.")
+
+
+@dataclass(frozen=True)
+class TonemapPlan:
+    """The branch decision of ``_tonemap_plan`` (src/ffmpeg_command.py:87-93,
+    :96-144), without its notices (UI, out of scope)."""
+    use_gpu: bool
+    dovi_needs_rpu: bool
+    use_libplacebo: bool
+
+
+def tonemap_plan(request: Any, properties: 'dict[str, Any] | None' = None,
+                 libplacebo_available: 'bool | Callable[[], bool]' = True) -> TonemapPlan:
+    """src/ffmpeg_command.py:96-144: bit_depth >= 12 turns ``use_gpu`` off
+    (no 12-bit hardware HEVC profile); Dolby Vision profile 5 needs the RPU
+    libplacebo applies, so it forces libplacebo even without ``use_gpu``;
+    the libplacebo probe is consulted only when one of the two asks for it
+    (the reference's laziness: a callable is called at most once, and only
+    then)."""
+    use_gpu = bool(getattr(request, 'use_gpu', False))
+    if int(getattr(request, 'bit_depth', 8)) >= 12:
+        use_gpu = False
+    props = properties or {}
+    dovi = bool(props.get('is_dolby_vision') and props.get('dovi_profile') == 5)
+    use_lp = False
+    if use_gpu or dovi:
+        use_lp = bool(libplacebo_available() if callable(libplacebo_available) else libplacebo_available)
+    return TonemapPlan(use_gpu=use_gpu, dovi_needs_rpu=dovi, use_libplacebo=use_lp)
+
+
 @dataclass(frozen=True)
 class TonemapParams:
     """Everything one kernel launch needs besides the LUT lattice.
@@ -110,7 +143,10 @@ class TonemapParams:
     # libplacebo branch options (include/h2s.h ABI v3; PARITY UNPINNED models)
     lp_range: str = 'full'      # what range=tv does to the rgba download ('full' | 'limited')
     lp_dither: str = 'none'     # the 8-bit download ('none' | 'ordered')
-    lp_p010: str = 'keep'       # 12-bit input through format=p010 ('keep' | 'truncate')
+    # 12-bit input through the upload prefix: 'truncate' = format=p010,hwupload
+    # (the reference's default, src/utils.py:431), 'keep' = the CUDA-interop
+    # hwmap=derive_device=vulkan prefix (:430)
+    lp_p010: str = 'truncate'
     # peak_detect=1 parameters (NaN: vf_libplacebo's defaults 100 / 5.5 / 10 / 99.995 / 1.0)
     pd_smoothing: float = math.nan
     pd_scene_low: float = math.nan
@@ -149,19 +185,46 @@ class TonemapParams:
     # ---- construction from the reference's request ---------------------
     @classmethod
     def from_request(cls, request: Any, bits_in: int = 10, transfer: str = 'smpte2084',
-                     **overrides: Any) -> 'TonemapParams':
-        """Map a ConversionRequest-like object (src/conversion.py:26-44).
+                     properties: 'dict[str, Any] | None' = None,
+                     libplacebo_available: 'bool | Callable[[], bool]' = True,
+                     cuda_interop: bool = False, **overrides: Any) -> 'TonemapParams':
+        """Map a ConversionRequest-like object (src/conversion.py:26-44) to
+        the params of the chain the reference's build() would emit for it.
 
-        * tonemapper: lower-cased as _filter_args does (src/ffmpeg_command.py:235).
-        * bit_depth -> output depth (src/ffmpeg_command.py:355-360; 8 -> yuv420p).
-        * lut_enabled: the CPU chain always applies the LUT
-          (src/utils.py:61-66 comment; construct_ffmpeg_command ignores it),
-          so it is honoured only when explicitly overridden.
-        """
+        * the branch: ``tonemap_plan`` (src/ffmpeg_command.py:96-144):
+          ``use_gpu`` sends every operator through libplacebo, bit_depth >= 12
+          forces the CPU chain, Dolby Vision profile 5 forces libplacebo;
+        * CPU chain (src/ffmpeg_command.py:240-247): bt.2390 / spline raise
+          ``ValueError`` with the reference's message; the LUT is always on
+          (``lut_enabled`` is ignored there, as ``_filter_args`` ignores it);
+        * libplacebo branch (``build_libplacebo_filter``, src/utils.py:392-471):
+          ``peak_detect=1`` always (:398, :448), ``lut_enabled`` honoured
+          (:435, :444, :451), and the upload prefix ``format=p010,hwupload``
+          (12-bit input cut to p010's 10 bits, ``lp_p010`` truncate) unless the
+          CUDA-interop ``hwmap`` prefix is used (``cuda_interop``: keep), :430-431;
+        * tonemapper lower-cased (src/ffmpeg_command.py:235); bit_depth ->
+          output depth (src/ffmpeg_command.py:355-360; 8 -> yuv420p).
+        ``properties`` / ``libplacebo_available`` are build()'s probe inputs
+        (``Probes.resolve_libplacebo_available``, src/ffmpeg_command.py:431-452):
+        the engine itself always runs the libplacebo branch natively, so the
+        default is True."""
+        plan = tonemap_plan(request, properties, libplacebo_available)
+        tm = str(request.tonemapper).lower()
         bit_depth = int(getattr(request, 'bit_depth', 8))
         bits_out = 12 if bit_depth >= 12 else (10 if bit_depth == 10 else 8)
-        kw = dict(tonemapper=str(request.tonemapper).lower(), gamma=float(request.gamma),
-                  bits_in=bits_in, bits_out=bits_out, transfer=transfer, lut_enabled=True)
+        kw: 'dict[str, Any]' = dict(tonemapper=tm, gamma=float(request.gamma), bits_in=bits_in,
+                                    bits_out=bits_out, transfer=transfer)
+        if plan.use_libplacebo:
+            if tm not in LIBPLACEBO_TONEMAPPERS:
+                raise ValueError(f'libplacebo tonemapping={tm} is not supported '
+                                 f'(the reference names {sorted(LIBPLACEBO_TONEMAPPERS)})')
+            kw.update(pipeline='libplacebo', desat=0.0, peak_detect=True,
+                      lut_enabled=bool(getattr(request, 'lut_enabled', True)),
+                      lp_p010='keep' if cuda_interop else 'truncate')
+        else:
+            if is_gpu_only_tonemapper(tm):
+                raise ValueError(CPU_GPU_ONLY_ERROR.format(tonemapper=tm))
+            kw.update(pipeline='cpu', lut_enabled=True)
         kw.update(overrides)
         return cls(**kw)
 
@@ -213,15 +276,42 @@ class TonemapParams:
         return 'libplacebo' if is_gpu_only_tonemapper(self.tonemapper) else 'cpu'
 
     # ---- back to the reference's chain string --------------------------
-    def filter_string(self, lut_path: str = '<LUT>') -> str:
-        """The CPU chain the reference would build for these params
-        (FFMPEG_CONVERT_FILTER.format, src/ffmpeg_command.py:246-247)."""
+    def filter_string(self, lut_path: str = '<LUT>', width: 'int | str' = 'iw', height: 'int | str' = 'ih') -> str:
+        """The chain the reference would build for these params: the CPU
+        chain (FFMPEG_CONVERT_FILTER.format, src/ffmpeg_command.py:246-247),
+        or for ``pipeline='libplacebo'`` the string of ``build_libplacebo_filter``
+        (src/utils.py:392-471) with the upload prefix ``lp_p010`` stands for
+        (truncate: ``format=p010,hwupload``; keep: the CUDA-interop ``hwmap``)."""
+        if self.pipeline == 'libplacebo':
+            return self._libplacebo_string(lut_path, width, height)
         if is_gpu_only_tonemapper(self.tonemapper):
             # src/ffmpeg_command.py:240-245
             raise ValueError(f"{self.tonemapper.lower()} requires GPU tonemapping; the reference CPU chain "
                              "has no equivalent")
         return FFMPEG_CONVERT_FILTER.format(gamma=self.gamma, tonemapper=self.tonemapper.lower(),
                                             lut_path=lut_path)
+
+    def _libplacebo_string(self, lut_path: str, width: 'int | str', height: 'int | str') -> str:
+        # the stage order and options of src/utils.py:426-471, composed from
+        # this engine's own fields (only the chain string is the interface)
+        interop = self.lp_p010 == 'keep'
+        lut = self.lut_enabled
+        fmt = 'rgba' if lut else 'nv12'
+        stage = (f'libplacebo=w={width}:h={height}:tonemapping={self.tonemapper.lower()}:colorspace=bt709:'
+                 f'color_primaries={"auto" if lut else "bt709"}:color_trc=bt709:range=tv:'
+                 f'peak_detect={1 if self.peak_detect else 0}:format={fmt}')
+        parts = ['hwmap=derive_device=vulkan' if interop else 'format=p010,hwupload', stage]
+        identity = abs(self.gamma - 1.0) < 1e-9
+        if lut:
+            parts += ['hwdownload', f'format={fmt}', f'lut3d=file={lut_path}:interp=tetrahedral',
+                      'setparams=color_primaries=bt709:color_trc=bt709:colorspace=bt709']
+        elif interop and identity:
+            parts += ['hwmap=reverse=1:derive_device=cuda']
+        else:
+            parts += ['hwdownload', 'format=nv12']
+        if not identity:
+            parts.append(f'eq=gamma={self.gamma}')
+        return ','.join(parts)
 
 
 _WRAP = re.compile(r'^\s*\[[^\]]*\](.*?)\[[^\]]*\]\s*$')
@@ -252,7 +342,11 @@ def _split_filters(chain: str) -> 'list[tuple[str, dict[str, str], list[str]]]':
 # and the values the engine models; anything else is rejected rather than
 # converted with a behaviour the string did not ask for
 _LP_OPTION_VALUES = {
-    'w': {'iw'}, 'h': {'ih'},                  # output size = input size (scaling is the preview's)
+    # output size: iw/ih, or the preview's numbers (extract_frame_with_gpu_conversion
+    # passes PREVIEW_SIZE, src/utils.py:787): the resize belongs to the Previewer
+    # (h2s_preview_rgb24), so any positive integer is accepted and the chain runs
+    # at the source size
+    'w': None, 'h': None,
     'colorspace': {'bt709'},
     'color_primaries': {'auto', 'bt709'},      # with / without the lut3d stage (checked after the loop)
     'color_trc': {'bt709'},
@@ -268,11 +362,14 @@ def _check_libplacebo_options(kv: 'dict[str, str]', pos: 'list[str]') -> None:
     for k, v in kv.items():
         if k == 'tonemapping':
             continue
-        allowed = _LP_OPTION_VALUES.get(k)
-        if allowed is None:
+        if k not in _LP_OPTION_VALUES:
             raise ValueError(f'libplacebo option {k}={v} is not modelled '
                              f'(the reference sets {sorted(_LP_OPTION_VALUES)} and tonemapping)')
-        if v not in allowed:
+        allowed = _LP_OPTION_VALUES[k]
+        if allowed is None:   # w / h
+            if v not in ('iw', 'ih') and not (v.isdigit() and int(v) > 0):
+                raise ValueError(f'libplacebo {k}={v} is not modelled (iw / ih or a positive integer)')
+        elif v not in allowed:
             raise ValueError(f'libplacebo {k}={v} is not modelled (accepted: {sorted(allowed)})')
 
 
@@ -293,6 +390,7 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
     lut_path = None
     seen_linear = False
     lp_primaries = lp_format = None
+    upload = None   # the libplacebo branch's upload prefix: 'p010' or 'hwmap' (src/utils.py:430-431)
     for name, kv, pos in _split_filters(chain):
         if name == 'zscale':
             t = kv.get('t', kv.get('transfer'))
@@ -353,7 +451,20 @@ def parse_filter_chain(chain: str, bits_in: int = 10, bits_out: int = 10,
                 kw['lp_range'] = 'full'          # full-range output: no model choice left
             lp_primaries = kv.get('color_primaries')
             lp_format = kv.get('format')
-        elif name in ('format', 'hwupload', 'hwdownload', 'hwmap', 'setparams'):
+            # format=p010,hwupload: the upload carries 10 bits, so 12-bit input
+            # loses its two low bits; the CUDA-interop hwmap prefix keeps them
+            if upload is not None:
+                kw['lp_p010'] = 'truncate' if upload == 'p010' else 'keep'
+        elif name == 'format':
+            fmt = kv.get('pix_fmts', pos[0] if pos else None)
+            if 'pipeline' not in kw:
+                upload = 'p010' if fmt == 'p010' else upload
+            continue  # the download's format=rgba / nv12 (src/utils.py:451-460)
+        elif name == 'hwmap':
+            if 'pipeline' not in kw and kv.get('derive_device') == 'vulkan':
+                upload = 'hwmap'
+            continue  # Vulkan -> CUDA remap after the stage (src/utils.py:463) moves no pixels
+        elif name in ('hwupload', 'hwdownload', 'setparams'):
             continue  # transfers / metadata-only retags (src/utils.py:21-29, :430-460)
         elif name == 'eq':
             if set(kv) - {'gamma'}:

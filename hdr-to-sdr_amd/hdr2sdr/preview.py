@@ -12,18 +12,29 @@ Here all of that is one libh2s call per frame: the chain through k_tile,
 the aspect-fit resize, the Y'CbCr -> RGB24 conversion and the display gamma,
 run on the GPU, with the RGB returned as an ``(h, w, 3)`` uint8 array.
 ``PIL.Image.fromarray`` takes that array directly.
+
+Which chain: the reference previews through libplacebo
+(``extract_frame_with_gpu_conversion``, src/utils.py:768-800: its
+``build_libplacebo_filter`` chain, so ``peak_detect=1`` and the LUT switch)
+for the GPU-only operators and whenever GPU tone mapping is on
+(``_use_gpu_extraction``, src/preview.py:584-590), and through
+FFMPEG_FILTER otherwise, where ``lut_enabled=False`` selects
+FFMPEG_FILTER_LEGACY_NO_LUT (src/utils.py:57-60).  ``convert_batch`` is the
+batched form (``extract_frames_with_conversion_batch`` /
+``extract_frames_with_gpu_conversion_batch``, src/utils.py:668-716, :803-824).
 """
 from __future__ import annotations
 
 import ctypes
 import math
-from typing import Any, Optional, Tuple
+import re
+from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _abi
 from . import lut as _lut
-from .chain import TonemapParams
+from .chain import TonemapParams, is_gpu_only_tonemapper, parse_filter_chain
 from .frames import FrameBatch
 
 PREVIEW_SIZE = (3840, 2160)   # src/preview.py:29
@@ -49,21 +60,86 @@ def adjust_gamma_lut(gamma: float) -> np.ndarray:
     return np.array([int(round(math.pow(i / 255.0, inv) * 255)) for i in range(256)], dtype=np.uint8)
 
 
+def use_gpu_extraction(tonemapper: str, gpu_tonemap_active: bool = False) -> bool:
+    """src/preview.py:584-590: the libplacebo preview for the GPU-only
+    operators, and for every operator while GPU tone mapping is on."""
+    return is_gpu_only_tonemapper(tonemapper) or bool(gpu_tonemap_active)
+
+
+def preview_params(tonemapper: str, lut_enabled: bool = True, use_gpu: bool = False, bits_in: int = 10,
+                   transfer: str = 'smpte2084', **params: Any) -> TonemapParams:
+    """The chain the reference's preview runs (gamma 1.0, yuv420p / rgba8
+    out): ``build_libplacebo_filter(1.0, tm, w, h, lut_enabled)`` — peak
+    detection on, the plain-Vulkan ``format=p010,hwupload`` upload — or
+    FFMPEG_FILTER (LUT always on) / FFMPEG_FILTER_LEGACY_NO_LUT."""
+    tm = tonemapper.lower()
+    kw: 'dict[str, Any]' = dict(tonemapper=tm, gamma=1.0, bits_in=bits_in, bits_out=8, transfer=transfer,
+                                lut_enabled=lut_enabled)
+    if use_gpu_extraction(tm, use_gpu):
+        kw.update(pipeline='libplacebo', desat=0.0, peak_detect=True, lp_p010='truncate')
+    else:
+        kw.update(pipeline='cpu')
+    kw.update(params)
+    return TonemapParams(**kw)
+
+
+def parse_preview_chain(chain: str, bits_in: int = 10, transfer: str = 'smpte2084',
+                        **overrides: Any) -> 'tuple[TonemapParams, str | None, tuple[int | str, int | str]]':
+    """A preview ``-vf`` string the reference builds -> (params, lut path, box).
+    FFMPEG_FILTER / FFMPEG_FILTER_LEGACY_NO_LUT end in
+    ``scale=W:H:force_original_aspect_ratio=decrease`` (src/utils.py:46-49,
+    :57-60); the libplacebo preview carries the box as its ``w=`` / ``h=``
+    (src/utils.py:787).  The box goes to ``Previewer.convert``; the chain
+    itself runs at the source size and bits_out 8."""
+    box: 'tuple[int | str, int | str]' = ('iw', 'ih')
+    parts = chain.rsplit(',', 1)
+    if len(parts) == 2 and parts[1].startswith('scale='):
+        opts = parts[1][len('scale='):].split(':')
+        kv = dict(o.split('=', 1) for o in opts[2:] if '=' in o)
+        if len(opts) < 2 or kv.get('force_original_aspect_ratio', 'decrease') != 'decrease':
+            raise ValueError(f'preview scale stage {parts[1]!r} is not the reference\'s aspect-fit box')
+        box = tuple(v if v in ('iw', 'ih') else int(v) for v in opts[:2])   # type: ignore[assignment]
+        chain = parts[0]
+    else:
+        m = re.search(r'libplacebo=w=(\w+):h=(\w+)', chain)
+        if m:
+            box = tuple(v if v in ('iw', 'ih') else int(v) for v in m.groups())   # type: ignore[assignment]
+    params, lut = parse_filter_chain(chain, bits_in=bits_in, bits_out=8, transfer=transfer, **overrides)
+    return params, lut, box
+
+
 class Previewer:
     """One libh2s context configured for previews. The chain runs at
     bits_out 8 with eq gamma 1.0, as extract_frame_with_conversion(gamma=1.0)
-    does. ``lut_enabled=False`` is the reference's FFMPEG_FILTER_LEGACY_NO_LUT
-    closed-form gamut path (src/utils.py:57-60)."""
+    and extract_frame_with_gpu_conversion(gamma=1.0) do. ``use_gpu``: GPU
+    tone mapping is on (the GUI's toggle, src/preview.py:570-582), which
+    selects the libplacebo preview for every operator; the GPU-only
+    operators take it regardless.  ``lut_enabled=False`` is
+    FFMPEG_FILTER_LEGACY_NO_LUT's closed-form gamut path on the CPU chain
+    (src/utils.py:57-60) and libplacebo's own BT.709 conversion on the GPU
+    one.  Each preview frame starts from a fresh peak state, as each of the
+    reference's preview ffmpeg runs does."""
 
     def __init__(self, device: int = 0, tonemapper: str = 'reinhard', lut_enabled: bool = True,
                  bits_in: int = 10, transfer: str = 'smpte2084', lattice: Optional[np.ndarray] = None,
-                 **params: Any):
+                 use_gpu: bool = False, params: Optional[TonemapParams] = None, **kw: Any):
         from .engine import Tonemapper
-        self.params = TonemapParams(tonemapper=tonemapper, gamma=1.0, bits_in=bits_in, bits_out=8,
-                                    transfer=transfer, lut_enabled=lut_enabled, **params)
+        if params is None:
+            params = preview_params(tonemapper, lut_enabled, use_gpu, bits_in, transfer, **kw)
+        elif params.bits_out != 8 or params.gamma != 1.0:
+            raise ValueError('a preview chain runs at bits_out 8 and gamma 1.0 (the display gamma is separate)')
+        self.params = params
+        lut_enabled = params.lut_enabled
         self._tm = Tonemapper(device, self.params)
         if lut_enabled:
             self._tm.set_lut(lattice if lattice is not None else _lut.generate_lattice(_lut.LUT_SIZE))
+
+    @classmethod
+    def from_chain(cls, chain: str, device: int = 0, bits_in: int = 10, transfer: str = 'smpte2084',
+                   lattice: Optional[np.ndarray] = None) -> 'tuple[Previewer, tuple[int | str, int | str]]':
+        """A Previewer for a reference preview ``-vf`` string, and its box."""
+        params, _, box = parse_preview_chain(chain, bits_in=bits_in, transfer=transfer)
+        return cls(device, lattice=lattice, params=params), box
 
     def close(self) -> None:
         self._tm.close()
@@ -79,14 +155,43 @@ class Previewer:
         """RGB24 preview of frame 0 of ``frame`` (host or device batch). width /
         height: the box (``'iw'``/``'ih'`` keep the source size, as in the
         reference's defaults). gamma: the GUI's display gamma, fused here."""
-        bw = frame.width if width == 'iw' else int(width)
-        bh = frame.height if height == 'ih' else int(height)
-        ow, oh = fit_size(frame.width, frame.height, bw, bh)
-        out = np.empty((oh, ow, 3), dtype=np.uint8)
-        d = frame.descriptor()
+        return self._run(frame.slice(0, 1) if frame.nframes > 1 else frame, width, height, gamma)[0]
+
+    def convert_batch(self, frames: 'FrameBatch | Sequence[FrameBatch]', width: 'int | str' = PREVIEW_SIZE[0],
+                      height: 'int | str' = PREVIEW_SIZE[1], gamma: float = 1.0) -> List[np.ndarray]:
+        """RGB24 previews of several frames: every frame of one FrameBatch, or
+        frame 0 of each batch in a list (frames of different sizes allowed).
+        Frames of one size run as one libh2s call (one tone-map launch on the
+        CPU chain; one resize and one RGB launch per plane either way)."""
+        if isinstance(frames, FrameBatch):
+            return self._run(frames, width, height, gamma)
+        out: 'list[np.ndarray | None]' = [None] * len(frames)
+        groups: 'dict[tuple[int, int, int, bool, Any], list[int]]' = {}
+        for i, f in enumerate(frames):
+            key = (f.width, f.height, f.bits, f.is_torch, getattr(f.buf, 'device', None))
+            groups.setdefault(key, []).append(i)
+        for idx in groups.values():
+            firsts = [frames[i] if frames[i].nframes == 1 else frames[i].slice(0, 1) for i in idx]
+            if firsts[0].is_torch:
+                import torch
+                buf = torch.cat([f.buf for f in firsts])
+            else:
+                buf = np.concatenate([np.asarray(f.buf) for f in firsts])
+            batch = FrameBatch(buf, firsts[0].width, firsts[0].height, firsts[0].bits)
+            for i, img in zip(idx, self._run(batch, width, height, gamma)):
+                out[i] = img
+        return out   # type: ignore[return-value]
+
+    def _run(self, frames: FrameBatch, width: 'int | str', height: 'int | str', gamma: float) -> List[np.ndarray]:
+        bw = frames.width if width == 'iw' else int(width)
+        bh = frames.height if height == 'ih' else int(height)
+        ow, oh = fit_size(frames.width, frames.height, bw, bh)
+        n = frames.nframes
+        out = np.empty((n, oh, ow, 3), dtype=np.uint8)
+        d = frames.descriptor()
         L = _abi.lib()
-        rc = L.h2s_preview_rgb24(self._tm._ctx, ctypes.byref(d), out.ctypes.data, 3 * ow, ow, oh, float(gamma),
-                                 _abi.LOC_HOST, self._tm._stream_ptr(None))
+        rc = L.h2s_preview_rgb24_batch(self._tm._ctx, ctypes.byref(d), n, out.ctypes.data, 3 * ow, 3 * ow * oh,
+                                       ow, oh, float(gamma), _abi.LOC_HOST, self._tm._stream_ptr(None))
         if rc:
             _abi.raise_for(rc, L.h2s_last_error(self._tm._ctx).decode())
-        return out
+        return [out[i] for i in range(n)]

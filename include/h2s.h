@@ -157,11 +157,12 @@ enum h2s_lp_tone { H2S_LP_TONE_IPT = 0, H2S_LP_TONE_MAX_RGB = 1 };
  *   16 x 16 Bayer matrix offsets each code before the truncation (a stand-in
  *   for libplacebo's default dither, whose blue-noise texture is not
  *   restated: it measures how much the dither matters).
- * h2s_lp_p010: the reference uploads through `format=p010` (src/utils.py:
- *   430-431).  KEEP = a 12-bit input reaches libplacebo at full precision
- *   (swscale's planar -> P01x path shifts the 12-bit code into the high bits,
- *   code << 4, and the low bits are read as fraction); TRUNCATE = the 10-bit
- *   container drops the two low bits (code & ~3).  10-bit input: no effect. */
+ * h2s_lp_p010: the upload prefix (src/utils.py:430-431).  TRUNCATE (the
+ *   default since ABI v3.1: the reference's default `format=p010,hwupload`
+ *   prefix) = the 10-bit p010 container drops a 12-bit input's two low bits
+ *   (code & ~3); KEEP = the CUDA-interop `hwmap=derive_device=vulkan` prefix,
+ *   which maps the decoder's frame without a format conversion, so 12-bit
+ *   input reaches libplacebo at full precision.  10-bit input: no effect. */
 enum h2s_lp_range { H2S_LP_RANGE_FULL = 0, H2S_LP_RANGE_LIMITED = 1 };
 enum h2s_lp_dither { H2S_LP_DITHER_NONE = 0, H2S_LP_DITHER_ORDERED = 1 };
 enum h2s_lp_p010 { H2S_LP_P010_KEEP = 0, H2S_LP_P010_TRUNCATE = 1 };
@@ -354,11 +355,23 @@ int h2s_peak_state(const h2s_ctx *ctx, double *max_pq, double *avg_pq, double *p
  *   limited Y'CbCr -> full-range RGB24 (nearest chroma), then the display
  *   gamma LUT round(255 (i/255)^(1/gamma)) on R, G, B (1.0 = identity).
  *   rgb: out_h rows of out_w*3 bytes, rgb_linesize apart, host or device per
- *   rgb_location.  Synchronous. */
+ *   rgb_location.  Synchronous.
+ * h2s_preview_rgb24_batch: the same for nframes frames of `in` (one size)
+ *   into nframes RGB images rgb_frame_pitch bytes apart — the reference's
+ *   batched preview (extract_frames_with_conversion_batch /
+ *   extract_frames_with_gpu_conversion_batch, src/utils.py:617-626,
+ *   :668-716, :803-824).  The CPU chain runs the batch as one tone-map
+ *   launch; with params.peak_detect (the libplacebo branch) each frame starts
+ *   from a fresh peak state, as each of the reference's per-frame ffmpeg runs
+ *   does.  The resize and RGB kernels take the whole batch in one launch each.
+ *   h2s_preview_rgb24 == the batch call with nframes = 1. */
 int h2s_preview_size(int in_w, int in_h, int box_w, int box_h, int *out_w, int *out_h);
 int h2s_preview_rgb24(h2s_ctx *ctx, const h2s_frames *in, uint8_t *rgb, int64_t rgb_linesize,
                       int out_w, int out_h, double display_gamma, int rgb_location,
                       void *hip_stream);
+int h2s_preview_rgb24_batch(h2s_ctx *ctx, const h2s_frames *in, int nframes, uint8_t *rgb,
+                            int64_t rgb_linesize, int64_t rgb_frame_pitch, int out_w, int out_h,
+                            double display_gamma, int rgb_location, void *hip_stream);
 
 /* ---- .cube helpers (tools/generate_lut.py:28-119; lut3d's .cube parser) --
  * h2s_cube_generate: the BT.2020->BT.709 lattice, n^3 triples, .cube order,

@@ -186,11 +186,17 @@ def debug_float(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, w
 
 def preview_rgb24(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
                   out_w: int, out_h: int, gamma: float = 1.0) -> np.ndarray:
-    """Preview of frame 0: the chain at bits_out 8, then the restated scale /
-    yuv420p->rgb24 / adjust_gamma tail (PARITY UNPINNED, see h2s_oracle.c)."""
+    """Preview of frame 0: the chain at bits_out 8 (with peak_detect: the
+    frame's own detected peak from a fresh state, as each of the reference's
+    preview ffmpeg runs starts one, src/utils.py:768-800), then the restated
+    scale / yuv420p->rgb24 / adjust_gamma tail (PARITY UNPINNED, see h2s_oracle.c)."""
     if params.bits_out != 8:
         raise ValueError('preview runs the chain at bits_out 8')
-    yuv8 = np.ascontiguousarray(process(params, lattice, np.ascontiguousarray(buf[:1]), width, height)[0])
+    one = np.ascontiguousarray(buf[:1])
+    if params.peak_detect:
+        yuv8 = np.ascontiguousarray(process_dynamic(params, lattice, one, width, height)[0][0])
+    else:
+        yuv8 = np.ascontiguousarray(process(params, lattice, one, width, height)[0])
     out = np.zeros((out_h, out_w, 3), dtype=np.uint8)
     rc = lib().oracle_preview_tail(yuv8.ctypes.data, width, height, out_w, out_h, float(gamma), out.ctypes.data)
     if rc:

@@ -13,8 +13,14 @@ strings) are written as JSON data.
                       BASELINE.json configurations C1..C5 (Appendix A of
                       SURVEY.md: stub tkinter, dummy ffmpeg on PATH, the LUT
                       regenerated into a temporary copy of src/).
+* request_rules.json — build() over a matrix of requests and probe results
+                      (use_gpu x operator x bit depth x lut_enabled x gamma,
+                      CUDA interop, Dolby Vision profile 5, libplacebo absent):
+                      the chain string or the ValueError it raises, plus the
+                      preview chains (FFMPEG_FILTER, build_libplacebo_filter
+                      with PREVIEW_SIZE) — pins TonemapParams.from_request.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [lut] [chains] [rules]   (default: all)
 """
 from __future__ import annotations
 
@@ -150,11 +156,113 @@ print(json.dumps(out))
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+RULES_SCRIPT = r'''
+import json, sys, os
+from dataclasses import dataclass
+sys.path.insert(0, os.path.join(sys.argv[1], 'src'))
+import utils, ffmpeg_command
+
+@dataclass(frozen=True)
+class Req:
+    input_path: str = 'in.mkv'
+    output_path: str = 'out.mkv'
+    gamma: float = 1.0
+    use_gpu: bool = False
+    tonemapper: str = 'reinhard'
+    quality: int = 23
+    quality_mode: str = 'cq'
+    bit_depth: int = 10
+    licensed: bool = False
+    lut_enabled: bool = True
+
+class View:
+    def notify(self, n): pass
+    def schedule(self, fn, *a): fn(*a)
+
+lut = utils.get_lut_filter_path()
+base_props = {'codec_name': 'hevc', 'frame_rate': 24.0, 'bit_rate': 8000000}
+cases = []
+for tm in ('reinhard', 'mobius', 'hable', 'bt.2390', 'spline'):
+    for use_gpu in (False, True):
+        for bd in (8, 10, 12):
+            cases.append(dict(req=dict(tonemapper=tm, use_gpu=use_gpu, bit_depth=bd, licensed=bd == 12)))
+for tm in ('hable', 'bt.2390'):
+    for lut_on in (True, False):
+        for g in (1.0, 2.2):
+            cases.append(dict(req=dict(tonemapper=tm, use_gpu=True, bit_depth=10, lut_enabled=lut_on, gamma=g)))
+            cases.append(dict(req=dict(tonemapper=tm, use_gpu=True, bit_depth=10, lut_enabled=lut_on, gamma=g),
+                              encoder='h264_nvenc', interop=True))
+    cases.append(dict(req=dict(tonemapper=tm, use_gpu=False, bit_depth=10, lut_enabled=False)))
+    cases.append(dict(req=dict(tonemapper=tm, use_gpu=True, bit_depth=10), libplacebo=False))
+    for bd in (10, 12):
+        cases.append(dict(req=dict(tonemapper=tm, use_gpu=False, bit_depth=bd, licensed=bd == 12),
+                          props=dict(is_dolby_vision=True, dovi_profile=5)))
+        cases.append(dict(req=dict(tonemapper=tm, use_gpu=False, bit_depth=bd, licensed=bd == 12),
+                          props=dict(is_dolby_vision=True, dovi_profile=8)))
+out = {'cases': []}
+for c in cases:
+    props = dict(base_props, **c.get('props', {}))
+    probes = ffmpeg_command.Probes(lambda c=c: c.get('encoder'), lambda c=c: c.get('libplacebo', True),
+                                   lambda c=c: c.get('interop', False))
+    r = Req(**c['req'])
+    rec = dict(c)
+    try:
+        argv = ffmpeg_command.build(r, props, probes, View())
+        fc = argv[argv.index('-filter_complex') + 1]
+        rec['filter_complex'] = fc.replace(lut, '<LUT>')
+        rec['pix_fmt'] = argv[argv.index('-pix_fmt') + 1]
+    except ValueError as e:
+        rec['error'] = str(e)
+    out['cases'].append(rec)
+prev = {}
+for tm in ('reinhard', 'mobius', 'hable'):
+    prev['cpu_' + tm] = utils.FFMPEG_FILTER.format(gamma=1.0, width=3840, height=2160, tonemapper=tm,
+                                                     lut_path='<LUT>')
+for tm in ('bt.2390', 'spline', 'hable'):
+    for lut_on in (True, False):
+        prev[f'gpu_{tm}_lut{int(lut_on)}'] = utils.build_libplacebo_filter(
+            1.0, tm, width=3840, height=2160, lut_enabled=lut_on).replace(lut, '<LUT>')
+out['preview'] = prev
+print(json.dumps(out))
+'''
+
+
+def rules_goldens() -> None:
+    tmp = tempfile.mkdtemp(prefix='h2s_refcopy_')
+    try:
+        shutil.copytree(os.path.join(REF, 'src'), os.path.join(tmp, 'src'))
+        shutil.copytree(os.path.join(REF, 'tools'), os.path.join(tmp, 'tools'))
+        subprocess.run([sys.executable, os.path.join(tmp, 'tools', 'generate_lut.py')], check=True,
+                       stdout=subprocess.DEVNULL)
+        fakebin = os.path.join(tmp, 'fakebin')
+        os.makedirs(fakebin)
+        for name in ('ffmpeg', 'ffprobe'):
+            p = os.path.join(fakebin, name)
+            with open(p, 'w') as f:
+                f.write('#!/bin/sh\nexit 1\n')
+            os.chmod(p, os.stat(p).st_mode | stat.S_IEXEC)
+        env = dict(os.environ, PATH=fakebin + os.pathsep + os.environ.get('PATH', ''))
+        res = subprocess.run([sys.executable, '-c', RULES_SCRIPT, tmp], env=env, check=True,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        data = json.loads(res.stdout.strip().splitlines()[-1])
+        data['source'] = ('src/ffmpeg_command.py build() over a request/probe matrix and src/utils.py '
+                          'FFMPEG_FILTER / build_libplacebo_filter preview chains (reference, imported)')
+        with open(os.path.join(HERE, 'request_rules.json'), 'w') as f:
+            json.dump(data, f, indent=1, sort_keys=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main() -> None:
+    only = sys.argv[1:]
     gen = load_generator()
-    lut_goldens(gen)
-    convert_goldens(gen)
-    chain_goldens()
+    if not only or 'lut' in only:
+        lut_goldens(gen)
+        convert_goldens(gen)
+    if not only or 'chains' in only:
+        chain_goldens()
+    if not only or 'rules' in only:
+        rules_goldens()
     print('golden fixtures written to', HERE)
 
 

@@ -55,3 +55,37 @@ def test_full_size_uniform_worst_case(tm):
 @pytest.mark.parametrize('cfg', ['C2_hable_pq10', 'C3_bt2390_libplacebo', 'C4_mobius_native', 'C5_hable_hlg12'])
 def test_tile_kernel_float_stages(tm, cfg, kind, stage):
     check_float_stage(tm, 'k_tile', cfg, kind, stage)
+
+
+def test_c3_as_the_reference_runs_it_4k_sequence(tm):
+    """C3 exactly as the reference's build() emits it for a BT.2390 request
+    with GPU tone mapping on (tests/golden/filter_chains.json C3:
+    format=p010,hwupload,libplacebo=...:peak_detect=1:format=rgba,...,lut3d):
+    five 4K frames of different brightness with a scene cut at frame 3,
+    through the captured chain's params (per-frame detected, temporally
+    smoothed peak), against the oracle's sequential model
+    (oracle.process_dynamic).  The frames carry MaxCLL 4000 so that the
+    detected peak moves instead of sitting at the 1000-nit default cap."""
+    import json
+    import os
+    import numpy as np
+    import oracle
+    from test_gpu_parity import lattice
+    from test_peak_detect import sequence
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'filter_chains.json')
+    with open(golden) as fh:
+        chain = json.load(fh)['C3']['filter_complex']
+    params, _ = hdr2sdr.parse_filter_chain(chain, bits_out=10, maxcll=4000.0)
+    assert params.peak_detect and params.resolved_pipeline() == 'libplacebo' and params.lp_p010 == 'truncate'
+    W, H = 3840, 2160
+    buf = sequence(W, H)[:5]
+    t = hdr2sdr.Tonemapper(0, params, lattice(65))
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)
+    dst = hdr2sdr.FrameBatch.empty_numpy(5, W, H, 10)
+    t.process(src, dst)
+    state = t.peak_state()
+    t.close()
+    want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert len(set(round(p, 3) for p in peaks)) >= 2, peaks        # the peak really moves
+    assert state['frames'] == 5 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
+    assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)

@@ -174,10 +174,18 @@ def test_libplacebo_reference_options_parse():
     _lp(extra=':percentile=99.9'),                     # peak-detect options are h2s_params fields, not parsed
     _lp().replace('color_trc=bt709', 'color_trc=smpte2084'),
     _lp().replace('colorspace=bt709', 'colorspace=bt2020nc'),
-    _lp().replace('w=iw', 'w=1920'),                   # scaling (the preview's job)
+    _lp().replace('w=iw', 'w=wide'),                   # a size expression libplacebo would evaluate
     _lp(prim='bt709'),                                 # libplacebo gamut mapping and the LUT: a double conversion
     _lp(prim='auto', fmt='nv12', lut=''),              # no gamut conversion at all
 ])
 def test_libplacebo_unmodelled_options_are_rejected(chain):
     with pytest.raises(ValueError):
         hdr2sdr.parse_filter_chain(chain)
+
+
+def test_libplacebo_numeric_size_is_the_previews_box():
+    """extract_frame_with_gpu_conversion passes PREVIEW_SIZE as w/h
+    (src/utils.py:787); the chain runs at the source size and the box goes to
+    the Previewer's resize."""
+    p, lut = parse_filter_chain(_lp().replace('w=iw:h=ih', 'w=3840:h=2160'))
+    assert p.resolved_pipeline() == 'libplacebo' and p.peak_detect and lut == '<LUT>'

@@ -85,6 +85,37 @@ def lattice_slope(n, s3):
     return out
 
 
+def parity_report(params, got, want, W, H, q, luma_within=None):
+    """Append one JSON line to $H2S_PARITY_REPORT (when set) with the shares
+    of output samples that agree exactly with the oracle, sit one quantiser
+    step off, and sit further off (a drift inside the
+    +-1 step / 0.5 % budget must be visible).  Luma with eq: 'one step'
+    means within eq[q-1] .. eq[q+1] of the oracle's code; everything else is
+    counted in output steps of the quantiser depth."""
+    import json
+    import os
+    path = os.environ.get('H2S_PARITY_REPORT')
+    if not path:
+        return None
+    step = 1 << max(0, params.bits_out - q)
+    ysz = W * H
+    d = np.abs(got - want)
+    dy, dc = d[:, :ysz], d[:, ysz:]
+    y_exact = float((dy == 0).mean())
+    y_one = float(luma_within.mean()) - y_exact if luma_within is not None else float(((dy > 0) & (dy <= step)).mean())
+    c_exact = float((dc == 0).mean())
+    c_one = float(((dc > 0) & (dc <= step)).mean())
+    rec = dict(test=os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0], pipeline=params.resolved_pipeline(),
+               tonemapper=params.tonemapper, bits_in=params.bits_in, bits_out=params.bits_out, gamma=params.gamma,
+               W=W, H=H, frames=int(got.shape[0]), quantiser_bits=q,
+               luma=dict(exact=y_exact, one_step=y_one, beyond=1.0 - y_exact - y_one),
+               chroma=dict(exact=c_exact, one_step=c_one, beyond=1.0 - c_exact - c_one),
+               max_diff_steps=int(d.max(initial=0) // step + (d.max(initial=0) % step > 0)))
+    with open(path, 'a') as fh:
+        fh.write(json.dumps(rec) + '\n')
+    return rec
+
+
 def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
     """Chroma: |diff| <= one quantisation step.  Luma: eq runs after the
     quantiser, so the bound is +-1 step *before* eq: got must lie between
@@ -105,6 +136,7 @@ def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
         k8 = math.ceil(_lattice_max_step(lut_n) * (lut_n - 1)) + 1
         bound = (math.ceil(k8 * 224 * (1 << (q - 8)) / 255) + 1) * step
         d = np.abs(got - want)
+        parity_report(params, got, want, W, H, q)
         assert d.max(initial=0) <= bound, f'max diff {d.max()} > {bound} ({k8} 8-bit R\'G\'B\' steps)'
         frac = float((d > step).mean())
         assert frac <= max_frac, f'{frac:.3%} of samples beyond one step'
@@ -127,6 +159,7 @@ def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
     lo = eq[np.clip(lo_i - 1, 0, len(eq) - 1)]
     hi = eq[np.clip(hi_i + 1, 0, len(eq) - 1)]
     bad = (gy < lo) | (gy > hi)
+    parity_report(params, got, want, W, H, q, luma_within=~bad)
     assert not bad.any(), f'{int(bad.sum())} luma samples beyond +-1 pre-eq step'
     # the fraction budget is for quantisers of <= 10 bits; a native 12-bit
     # LSB is 4x finer, so the same float-level disagreement flips 4x as often

@@ -178,3 +178,42 @@ def test_gpu_lut_chain_tracks_legacy_gamut_chain(kind, seed):
     d = np.abs(legacy[ys][:, xs] - with_lut[ys][:, xs])
     assert d.max() <= 12, f'LUT chain differs from the legacy chain by up to {d.max()}/255'
     assert np.abs(legacy - with_lut).mean() < 3.0        # and close on average, not only on the grid
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tm,use_gpu', [('reinhard', False), ('bt.2390', False), ('hable', True)])
+def test_gpu_preview_batch_mixed_sizes_vs_oracle(tm, use_gpu):
+    """The batched preview (extract_frames_with_conversion_batch /
+    extract_frames_with_gpu_conversion_batch, src/utils.py:668-716, :803-824):
+    N = 4 frames of two sizes in one convert_batch call (one libh2s call per
+    size), each against the oracle's chain + preview tail for that frame
+    alone, and bit-identical to converting it on its own.  The libplacebo
+    preview (bt.2390; hable with GPU tone mapping on) detects each frame's
+    peak from a fresh state, as the reference's per-frame ffmpeg runs do."""
+    sizes = [(256, 128), (384, 256), (256, 128), (384, 256)]
+    frames = [synth_frames('smooth', 1, w, h, 10, device='cpu', seed=60 + i).to_numpy()
+              for i, (w, h) in enumerate(sizes)]
+    box = (192, 108)
+    with PV.Previewer(0, tonemapper=tm, use_gpu=use_gpu, lattice=_lat()) as pv:
+        assert pv.params.peak_detect == (tm == 'bt.2390' or use_gpu)
+        batch = pv.convert_batch(frames, *box, gamma=1.3)
+        singles = [pv.convert(f, *box, gamma=1.3) for f in frames]
+        op = oracle.params_from(pv.params.to_c())
+    for f, (w, h), got, one in zip(frames, sizes, batch, singles):
+        ow, oh = PV.fit_size(w, h, *box)
+        assert got.shape == (oh, ow, 3)
+        assert np.array_equal(got, one)
+        want = oracle.preview_rgb24(op, _lat(), f.buf, w, h, ow, oh, 1.3)
+        d = np.abs(got.astype(int) - want.astype(int))
+        assert d.max() <= 4 and (d > 1).mean() < 1e-2
+
+
+@pytest.mark.gpu
+def test_gpu_preview_batch_one_size_is_one_frame_batch():
+    """Frames of one FrameBatch go through as one batch: equal to their
+    single-frame previews."""
+    src = synth_frames('smooth', 3, 256, 128, 10, device='cpu', seed=9).to_numpy()
+    with PV.Previewer(0, tonemapper='hable', lattice=_lat()) as pv:
+        batch = pv.convert_batch(src, 'iw', 'ih')
+        singles = [pv.convert(src.slice(i, i + 1), 'iw', 'ih') for i in range(3)]
+    assert len(batch) == 3 and all(np.array_equal(a, b) for a, b in zip(batch, singles))

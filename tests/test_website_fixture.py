@@ -218,13 +218,16 @@ def test_hip_path_with_reference_c3_settings():
 @pytest.mark.gpu
 def test_hip_preview_path_on_the_website_pair():
     """The product path (h2s_preview_rgb24 on cuda:0, k_tile<..., LP>) on the
-    same pair: the oracle's pixels within one 8-bit step, and the same fit
-    (the preview decodes BT.709: the 'bt2020' screenshot model)."""
+    same pair, as the reference previews it (extract_frame_with_gpu_conversion:
+    build_libplacebo_filter, so peak_detect=1 from a fresh state): the
+    oracle's pixels within one 8-bit step, and the same fit (the preview
+    decodes BT.709: the 'bt2020' screenshot model)."""
     from hdr2sdr import preview as PV
     fb, sdr = fixture_frame('bt2020')
-    with PV.Previewer(0, tonemapper='bt.2390', peak=8.0, lattice=lattice()) as pv:
+    with PV.Previewer(0, tonemapper='bt.2390', lattice=lattice()) as pv:
+        assert pv.params.peak_detect and pv.params.resolved_pipeline() == 'libplacebo'
         got = pv.convert(fb, 'iw', 'ih').astype(np.int32)
-    p = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak=8.0, bits_out=8)
+        p = pv.params
     want = oracle.preview_rgb24(oracle.params_from(p.to_c()), lattice(), fb.buf, fb.width, fb.height,
                                 fb.width, fb.height).astype(np.int32)
     assert (np.abs(got - want) <= 1).mean() > 0.99
