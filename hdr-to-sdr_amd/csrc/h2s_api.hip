@@ -72,6 +72,7 @@ struct h2s_ctx {
   double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
   long long pk_frames = 0;
   std::string err;
+  bool fail_after_launch = false;  // H2S_OPT_FAIL_AFTER_LAUNCH (test hook, one call)
   bool timing = false;
   hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
   long long ev_count = 0;  // launches recorded since reset
@@ -801,6 +802,20 @@ static hipError_t table_copy(h2s_ctx* c, void* dst, const void* src, size_t byte
   return e == hipSuccess ? hipStreamSynchronize(c->aux) : e;
 }
 
+static int note_launch(h2s_ctx* c, hipStream_t s);
+
+// an error exit of h2s_process after work was queued on s: record the launch
+// event anyway, so that a later set_params / set_lut still waits for that work
+// before rewriting the tables it reads (include/h2s.h); if even the event
+// cannot be recorded, wait for the stream.  The caller's error stays the one
+// reported.
+static int queued_exit(h2s_ctx* c, hipStream_t s, int rc) {
+  const std::string msg = c->err;
+  if (note_launch(c, s) != 0) (void)hipStreamSynchronize(s);
+  c->err = msg;
+  return rc;
+}
+
 // record that this context queued work on stream s (after the launches)
 static int note_launch(h2s_ctx* c, hipStream_t s) {
   if (c->pend.size() >= 32) {   // recycle the events that have completed
@@ -1055,7 +1070,13 @@ static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
   if (!c->d_lut_yuv) {  // beside d_lut: stream-ordered on the context stream, complete before s uses it
     hipStream_t aux;
     if (int rc = aux_stream(c, &aux)) return rc;
-    hipError_t e = hipMallocAsync((void**)&c->d_lut_yuv, cnt * 3 * sizeof(float) + 16, aux);
+    // zero-filled tail: a coordinate clamped to exactly N-1 (k_tile's
+    // H2S_EXPCLAMP form) names cell N-1, whose corners past the lattice edge
+    // carry weight 0 but are still read; the scalar-record steps read them
+    // without the buffer resource's bounds check, so they must be mapped
+    const size_t pad = 12 * (1 + (size_t)c->lut_n + (size_t)c->lut_n * c->lut_n) + 16;
+    hipError_t e = hipMallocAsync((void**)&c->d_lut_yuv, cnt * 3 * sizeof(float) + pad, aux);
+    if (e == hipSuccess) e = hipMemsetAsync((uint8_t*)c->d_lut_yuv + cnt * 3 * sizeof(float), 0, pad, aux);
     if (e == hipSuccess) e = hipStreamSynchronize(aux);
     if (e != hipSuccess) {
       c->d_lut_yuv = nullptr;
@@ -1619,7 +1640,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     return process_pipelined(c, k, in, out, din, dout, nframes, fast, vec, out8, s);
   if (host_in) {
     hipError_t e = copy_frames(&din, in, nframes, s);
-    if (e != hipSuccess) return hip_fail(c, e, "host->device copy");
+    if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "host->device copy"));
   }
   const int slot = (int)(c->ev_count % kEvRing);
   if (c->timing) {
@@ -1631,27 +1652,31 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   }
   hipError_t e;
   if (dyn_peak) {
-    if ((rc = run_dynamic_peak(c, k, fast, vec, out8, nframes, s))) return rc;
+    if ((rc = run_dynamic_peak(c, k, fast, vec, out8, nframes, s))) return queued_exit(c, s, rc);
     e = hipSuccess;
   } else {
     e = launch_chain(c, k, fast, vec, out8, nframes, s);
   }
-  if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+  if (e == hipSuccess && c->fail_after_launch) {
+    c->fail_after_launch = false;
+    return queued_exit(c, s, fail(c, H2S_E_HIP, "injected failure after the launch (H2S_OPT_FAIL_AFTER_LAUNCH)"));
+  }
+  if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "kernel launch"));
   if (c->timing) {
     hipEventRecord(c->ev1[slot], s);
     c->ev_count++;
   }
   if (host_out) {
     e = copy_frames(out, &dout, nframes, s);
-    if (e != hipSuccess) return hip_fail(c, e, "device->host copy");
+    if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "device->host copy"));
   }
   if (two_pass) {
-    if ((e = hipEventRecord(c->chr_ev, s)) != hipSuccess) return hip_fail(c, e, "two-pass event");
+    if ((e = hipEventRecord(c->chr_ev, s)) != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "two-pass event"));
     c->chr_pending = true;
   }
   if (host_in || host_out) {
     e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(c, e, "stream synchronize");
+    if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "stream synchronize"));
     return 0;
   }
   return note_launch(c, s);
@@ -1723,6 +1748,9 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
       return 0;
     case H2S_OPT_HOST_SERIAL:
       c->serial_host = value != 0;
+      return 0;
+    case H2S_OPT_FAIL_AFTER_LAUNCH:
+      c->fail_after_launch = value != 0;
       return 0;
     default:
       return fail(c, H2S_E_INVALID_ARG, "unknown option");

@@ -35,7 +35,8 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
     yuv[3 * i] = c.x, yuv[3 * i + 1] = c.y, yuv[3 * i + 2] = c.z;
     return;
   }
-  yuv[3 * i] = (16.0f + 219.0f * Y) * s + 0.5f;
+  // (H2S_EQMAGIC: no +0.5, k_tile rounds to nearest instead)
+  yuv[3 * i] = (16.0f + 219.0f * Y) * s + (H2S_EQMAGIC ? 0.0f : 0.5f);
   yuv[3 * i + 1] = 224.0f * s * 0.25f * cb;
   yuv[3 * i + 2] = 224.0f * s * 0.25f * cr;
 }

@@ -355,9 +355,26 @@ __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned
 // a PEAK_BINS-bin histogram of the per-pixel PQ(max R,G,B) per frame; the
 // host interpolates the percentile inside its bin (oracle_peak_stats)
 constexpr int PEAK_BINS = 1024;
-__device__ __forceinline__ void hist_add(unsigned* lh, float m) {
-  atomicAdd(&lh[min((int)(m * (float)PEAK_BINS), PEAK_BINS - 1)], 1u);
-}
+// a thread's run of equal bins, added to the LDS histogram once per run: on
+// smooth content neighbouring pixels share a bin, and one LDS atomic per pixel
+// had all 64 lanes of a wave serialise on one address; the
+// counts are the same, only the number of atomics changes
+struct HistRun {
+  int bin = -1;
+  unsigned n = 0;
+  __device__ __forceinline__ void add(unsigned* lh, float m) {
+    const int b = min((int)(m * (float)PEAK_BINS), PEAK_BINS - 1);
+    if (b != bin) {
+      if (n) atomicAdd(&lh[bin], n);
+      bin = b, n = 0;
+    }
+    n++;
+  }
+  __device__ __forceinline__ void flush(unsigned* lh) {
+    if (n) atomicAdd(&lh[bin], n);
+    n = 0;
+  }
+};
 __device__ __forceinline__ void hist_flush(const unsigned* lh, unsigned* hist) {
   __syncthreads();
   for (int i = threadIdx.x; i < PEAK_BINS; i += 256)
@@ -388,6 +405,7 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
   if (HIST) __syncthreads();
   const int f = blockIdx.y, b = blockIdx.x;
   float mx = 0.0f, sm = 0.0f;
+  HistRun run;
   for (int y = b; y < P.H; y += gridDim.x) {
     const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
     const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
@@ -397,10 +415,11 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
       const float m = peak_px<TRC>(P, yr[x], ur[x >> 1], vr[x >> 1]);
       mx = fmaxf(mx, m);
       rs += m;
-      if (HIST) hist_add(lh, m);
+      if (HIST) run.add(lh, m);
     }
     sm += rs;
   }
+  if (HIST) run.flush(lh);
   if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
   peak_reduce(mx, sm, &partial[f * gridDim.x + b]);
 }
@@ -421,6 +440,7 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
   const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
   const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
   float mx = 0.0f, sm = 0.0f;
+  HistRun run;
   auto chunk = [&](int i, uint4& ya, uint2& ua, uint2& va) {
     const int y = i / cpr, cx = i - y * cpr;
     ya = reinterpret_cast<const uint4*>(y0 + y * P.in_ls[0])[cx];
@@ -438,7 +458,7 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
       const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
       mx = fmaxf(mx, m);
       rs += m;
-      if (HIST) hist_add(lh, m);
+      if (HIST) run.add(lh, m);
     }
     sm += rs;
   };
@@ -457,6 +477,7 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
     chunk(i, ya, ua, va);
     fold(ya, ua, va);
   }
+  if (HIST) run.flush(lh);
   if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
   peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
 }

@@ -31,6 +31,28 @@
 
 #include "h2s_device.h"
 
+// Round-4 VALU trims of the step (on by default, each
+// switchable for A/B builds, scripts/build_variants.sh):
+//  H2S_TAGSEL    tetrahedron from axis-tagged fractions + a 3-entry LDS
+//                offset table, one-key uniformity test (9 + 6 half-rate ops -> 6)
+//  H2S_EXPCLAMP  lut3d's [0, N-1] clamp as v_exp_f32's output clamp
+//  H2S_EQMAGIC   eq index by a 2^23 add and a 16-bit shift (full-rate ops)
+//  H2S_DARKEXACT exact EOTF for channels in the PQ table's first segment,
+//                ballot-gated per step (off: +15 % on the website frame,
+//                the per-step branch breaks the straight-line fast body)
+#ifndef H2S_TAGSEL
+#define H2S_TAGSEL 1
+#endif
+#ifndef H2S_EXPCLAMP
+#define H2S_EXPCLAMP 1
+#endif
+#ifndef H2S_EQMAGIC
+#define H2S_EQMAGIC 1
+#endif
+#ifndef H2S_DARKEXACT
+#define H2S_DARKEXACT 0
+#endif
+
 namespace h2s {
 
 typedef float f3 __attribute__((ext_vector_type(3)));
@@ -109,16 +131,30 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
     // E arrives as E*PQ_SEG + 1 (pq_z)
     static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
     r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
-    if (NOEX) return false;
-    const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
     constexpr float EI = 1.0f / (float)PQ_SEG;
-    if (__builtin_amdgcn_ballot_w64(emax >= PQZ_LIM)) {  // rare: extreme out-of-gamut codes
-      r = er >= PQZ_LIM ? pq_exact(F, (er - 1.0f) * EI) : r;
-      g = eg >= PQZ_LIM ? pq_exact(F, (eg - 1.0f) * EI) : g;
-      b = eb >= PQZ_LIM ? pq_exact(F, (eb - 1.0f) * EI) : b;
-      return true;
+    // NOEX (the fast body): the tile's codes keep every E inside the table
+    // (tflag) and, with H2S_DARKEXACT, out of its first segment (tdark)
+    if (NOEX) return false;
+#if H2S_DARKEXACT
+    // the table's first segment (E < 1/128, staged u < 2: below ~0.0015
+    // nits) is where EOTF ~ (E - E0)^6.28 and no cubic in t holds 1e-3
+    // relative; a wave with such a channel evaluates those channels exactly
+    // (zimg's formula).  Only tiles whose code ranges allow such a channel
+    // get here (k_tile's tdark bound; about 1 % of the bench content's 8x8
+    // steps hold one)
+    const float emin = __builtin_fminf(__builtin_fminf(er, eg), eb);
+    const bool dark = __builtin_amdgcn_ballot_w64(emin < 2.0f) != 0;
+#else
+    const bool dark = false;
+#endif
+    const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
+    const bool high = __builtin_amdgcn_ballot_w64(emax >= PQZ_LIM) != 0;   // rare: extreme out-of-gamut codes
+    if (high || dark) {
+      r = er >= PQZ_LIM || er < 2.0f ? pq_exact(F, (er - 1.0f) * EI) : r;
+      g = eg >= PQZ_LIM || eg < 2.0f ? pq_exact(F, (eg - 1.0f) * EI) : g;
+      b = eb >= PQZ_LIM || eb < 2.0f ? pq_exact(F, (eb - 1.0f) * EI) : b;
     }
-    return false;
+    return high;
   } else {
     // zimg arib_b67_inverse_oetf, branch-free; then the OOTF (gamma 1.2)
     auto inv = [](float e) -> float {
@@ -359,6 +395,9 @@ struct StepK {
   int og, ob, ocr, ocg, ocb;      // corner byte offsets
   float log2_nm1, x_max;
   float hable_kb;                 // F.hable_kb (Hable instances)
+  int c111;                       // the far corner's byte offset
+  float nm1;                      // N - 1
+  const int* offtab;              // LDS: byte offset of the +1 corner along r, g, b at bytes 0, 4, 8
 };
 
 // One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
@@ -374,6 +413,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
   // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
+  constexpr bool EQM = H2S_EQMAGIC && !LP;   // see the eq lookup at the end
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
   const float eb = fmaf(U, K.a_bu, ybs);
@@ -401,7 +441,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     const float B = enc(F.m709[6] * r + F.m709[7] * gg + F.m709[8] * bl);
     if (DBG == 3 || DBG == 4) dput(R, G, B);
     const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, 0.5f + ydq);
+    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
     o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
     o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
   } else {
@@ -428,18 +468,60 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     } else {
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, K.x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
+#if H2S_EXPCLAMP
+      // lut3d's clamp to [0, N-1] (NaN -> 0) as the exp's output clamp:
+      // x^(1/2.4) clamped to [0, 1] (v_exp_f32 ... clamp; a NaN from the log
+      // of a negative or NaN x clamps to 0), then N - 1 times that.  s may
+      // reach N-1 exactly: its corners past the lattice edge get weight 0
+      // (zero fraction), and the lattice allocation is padded for them
+      sr = __builtin_amdgcn_fmed3f(fexp2(flog2(r) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
+      sg = __builtin_amdgcn_fmed3f(fexp2(flog2(gg) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
+      sb = __builtin_amdgcn_fmed3f(fexp2(flog2(bl) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
+#else
       sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
       sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
       sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
+#endif
     }
     const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
     const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * 12.0f));
-    const bool rg = dr > dg, gb = dg > db, rb = dr > db;
-    const int om = rg ? (rb ? 12 : K.ob) : (gb ? K.og : K.ob);
-    const int ocn = rg ? (gb ? K.ocb : K.ocg) : (rb ? K.ocb : K.ocr);
-    const float dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
-    const float dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
-    const float dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
+    // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
+    // fractions: the 4 low mantissa bits of each fraction carry its axis a
+    // (bits 3:2 and 1:0 both = a; r 0, g 1, b 2; a change of <= 2^-19
+    // relative in the weights), so max3 / min3 / med3 of the bit patterns
+    // (non-negative floats order as integers) give the sorted fractions and
+    // the axes of the largest and smallest; the corner offsets come from a
+    // 3-entry LDS table (om = +1 along the max axis, ocn = the far corner less
+    // the min axis), not from compares and selects (9 half-rate VALU ops ->
+    // 3).  Not on the libplacebo branch: its 8-bit coordinates make exact ties
+    // between fractions common, and lut3d's truncating 8-bit output turns the
+    // tags' perturbation of a tie into a flipped code (1.3 % of a ramp's
+    // pixels)
+    constexpr bool TAG = H2S_TAGSEL && !LP;
+    int om, ocn;
+    float dmax, dmin, dmid;
+    unsigned umin = 0, amax = 0;
+    if constexpr (TAG) {
+      const unsigned ur = __builtin_bit_cast(unsigned, dr) & ~15u;
+      const unsigned ug = (__builtin_bit_cast(unsigned, dg) & ~15u) | 5u;
+      const unsigned ub = (__builtin_bit_cast(unsigned, db) & ~15u) | 10u;
+      unsigned umax, umid;
+      asm("v_max3_u32 %0, %1, %2, %3" : "=v"(umax) : "v"(ur), "v"(ug), "v"(ub));
+      asm("v_min3_u32 %0, %1, %2, %3" : "=v"(umin) : "v"(ur), "v"(ug), "v"(ub));
+      asm("v_med3_u32 %0, %1, %2, %3" : "=v"(umid) : "v"(ur), "v"(ug), "v"(ub));
+      amax = umax & 12u;
+      const unsigned amin = umin & 12u;
+      om = *reinterpret_cast<const int*>(reinterpret_cast<const char*>(K.offtab) + amax);
+      ocn = K.c111 - *reinterpret_cast<const int*>(reinterpret_cast<const char*>(K.offtab) + amin);
+      dmax = __builtin_bit_cast(float, umax), dmin = __builtin_bit_cast(float, umin), dmid = __builtin_bit_cast(float, umid);
+    } else {
+      const bool rg = dr > dg, gb = dg > db, rb = dr > db;
+      om = rg ? (rb ? 12 : K.ob) : (gb ? K.og : K.ob);
+      ocn = rg ? (gb ? K.ocb : K.ocg) : (rb ? K.ocb : K.ocr);
+      dmax = __builtin_fmaxf(__builtin_fmaxf(dr, dg), db);
+      dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
+      dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
+    }
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     auto blend = [&](const f3 c0, const f3 c1, const f3 c2, const f3 c3) {
       f3 r = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
@@ -455,9 +537,26 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     // step issues no vector-memory gather (bit-identical; C2 -1.8 % smooth,
     // -5 % on the website frame; the libplacebo instances measured +8 %,
     // SGPR-bound, and keep the gathers: profiles/r03/ablations/sgather_*.log)
-    const int b0 = __builtin_amdgcn_readfirstlane(base), m0 = __builtin_amdgcn_readfirstlane(om),
-              n0 = __builtin_amdgcn_readfirstlane(ocn);
-    if (!LP && __builtin_amdgcn_ballot_w64(base != b0 || om != m0 || ocn != n0) == 0) {
+    bool step_uniform;
+    int b0, m0, n0;
+    if constexpr (TAG) {
+      // one key per lane: cell (base) and tetrahedron (the max and min axes)
+      unsigned tkey, key;
+      asm("v_and_or_b32 %0, %1, 3, %2" : "=v"(tkey) : "v"(umin), "v"(amax));
+      asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(key) : "v"(base), "v"(tkey));
+      const unsigned key0 = __builtin_amdgcn_readfirstlane(key);
+      step_uniform = __builtin_amdgcn_ballot_w64(key != key0) == 0;
+      b0 = 0, m0 = 0, n0 = 0;
+      if (step_uniform) {
+        b0 = (int)(key0 >> 4);
+        m0 = __builtin_amdgcn_readfirstlane(om), n0 = __builtin_amdgcn_readfirstlane(ocn);
+      }
+    } else {
+      b0 = __builtin_amdgcn_readfirstlane(base), m0 = __builtin_amdgcn_readfirstlane(om),
+      n0 = __builtin_amdgcn_readfirstlane(ocn);
+      step_uniform = !LP && __builtin_amdgcn_ballot_w64(base != b0 || om != m0 || ocn != n0) == 0;
+    }
+    if (step_uniform) {
       typedef __attribute__((address_space(4))) const float cfl;
       cfl* L = (cfl*)F.lut_yuv;
       auto sl = [&](int off) {
@@ -478,7 +577,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       const float B = __builtin_amdgcn_fmed3f(truncf(o.z * 255.0f), 0.0f, 255.0f) * F.inv255;
       if (DBG == 4) dput(R, G, B);
       const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-      o.x = fmaf(16.0f + 219.0f * Y, F.qscale, 0.5f + ydq);
+      o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
       o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
       o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
     }
@@ -490,9 +589,22 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
            w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
     }
   }
-  if (DBG == 5) dput(o.x - 0.5f - ydq, 4.0f * o.y, 4.0f * o.z);
+  if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
-  return eq_lds[(int)o.x];
+  if constexpr (EQM) {
+    // o.x = the luma quantiser input less 0.5 (the lattice records carry no
+    // +0.5): adding 2^23 rounds it to the nearest integer in the mantissa's
+    // low bits, and a 16-bit shift turns that into the table's byte offset
+    // (two full-rate ops instead of a conversion and a 32-bit shift-add; an
+    // exact .5 tie rounds to even instead of up: continuous blends of the
+    // CPU chain, not the libplacebo branch's 8-bit-derived values)
+    const unsigned qb = __builtin_bit_cast(unsigned, o.x + 8388608.0f);
+    unsigned off;
+    asm("v_lshlrev_b16 %0, 1, %1" : "=v"(off) : "v"(qb));
+    return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(eq_lds) + off);
+  } else {
+    return eq_lds[(int)o.x];
+  }
 }
 
 constexpr int CBW = 32, CBH = 16;  // chroma tile
@@ -639,6 +751,22 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
   return r;
 }
 
+// smallest / largest of the 8 u16 codes packed in a 16-byte chunk
+__device__ __forceinline__ unsigned min8_u16(uint4 a) {
+  unsigned m, n, o;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(a.x), "v"(a.y));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(n) : "v"(a.z), "v"(a.w));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(o) : "v"(m), "v"(n));
+  return min(o & 0xFFFFu, o >> 16);
+}
+__device__ __forceinline__ unsigned max8_u16(uint4 a) {
+  unsigned m, n, o;
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(m) : "v"(a.x), "v"(a.y));
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(n) : "v"(a.z), "v"(a.w));
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(o) : "v"(m), "v"(n));
+  return max(o & 0xFFFFu, o >> 16);
+}
+
 // staging and store helpers of k_tile
 // 8 luma samples -> Y*ys + y_off floats at (row, 8 col8)
 // returns the largest staged value
@@ -761,6 +889,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
+  __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
+  __shared__ int tdark[2][5];                  // per tile parity: min luma, min/max U, min/max V codes (H2S_DARKEXACT)
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -793,6 +923,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
+  if (t < 10) tdark[t / 5][t % 5] = (t % 5) == 2 || (t % 5) == 4 ? 0 : 0x7FFFFFFF;
+  if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
   __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
     const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
@@ -824,7 +956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
   const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
-                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb};
+                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab};
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
@@ -893,6 +1025,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     if ((t & 127) < 72) mc = stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
     const int par = (int)(tile & 1u);
     if ((my > F.safe_y || mc > F.safe_c)) tflag[par] = 1;
+    if (H2S_DARKEXACT && TRC == 0) {
+      // the tile's smallest luma and the range of each chroma plane (raw
+      // codes), for the bound that keeps dark channels out of the fast body
+      atomicMin(&tdark[par][0], (int)min8_u16(cur.ya));
+      if ((t & 127) < 72) {
+        const int pc = (t >> 7) & 1;
+        const unsigned h = cur.uh;
+        atomicMin(&tdark[par][1 + 2 * pc], (int)min(min8_u16(cur.ua), h));
+        atomicMax(&tdark[par][2 + 2 * pc], (int)max(max8_u16(cur.ua), h));
+      }
+    }
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
@@ -900,8 +1043,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
       cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
     __syncthreads();
-    const bool fb = __builtin_amdgcn_readfirstlane(tflag[par]) == 0 && !F.chr444;
+    bool fb = __builtin_amdgcn_readfirstlane(tflag[par]) == 0 && !F.chr444;
     if (t == 0) tflag[par ^ 1] = 0;   // for the next tile: read by every wave of the previous one before this barrier
+    if (H2S_DARKEXACT && TRC == 0) {
+      // lower bound of every pixel's E (staged units) over the tile: E_c =
+      // Y' + the channel's chroma terms, each at its extreme; a bound below
+      // the table's first segment sends the tile to the checked body
+      const float ymn = (float)__builtin_amdgcn_readfirstlane(tdark[par][0]) * ysc + yoff;
+      const float ulo = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][1]) - cmid);
+      const float uhi = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][2]) - cmid);
+      const float vlo = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][3]) - cmid);
+      const float vhi = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][4]) - cmid);
+      const float elo = __builtin_fminf(__builtin_fminf(fmaf(a_rv, vlo, ymn), fmaf(a_bu, ulo, ymn)),
+                                        fmaf(a_gv, vhi, fmaf(a_gu, uhi, ymn)));   // a_rv, a_bu > 0 > a_gu, a_gv
+      fb = fb && !(elo < 2.0f);
+      if (t < 5) tdark[par ^ 1][t] = t == 2 || t == 4 ? 0 : 0x7FFFFFFF;
+    }
     if (fb)
       steps(g, std::integral_constant<bool, true>{});
     else

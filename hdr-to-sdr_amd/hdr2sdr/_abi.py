@@ -38,7 +38,7 @@ LP_RANGE_FULL, LP_RANGE_LIMITED = 0, 1
 LP_DITHER_NONE, LP_DITHER_ORDERED = 0, 1
 LP_P010_KEEP, LP_P010_TRUNCATE = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
-OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
+OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL, OPT_FAIL_AFTER_LAUNCH = 1, 2, 3, 4
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
 ABI_VERSION = 3
 

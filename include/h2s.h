@@ -189,7 +189,9 @@ enum h2s_pipeline { H2S_PIPE_AUTO = 0, H2S_PIPE_CPU_CHAIN = 1, H2S_PIPE_LIBPLACE
 enum h2s_option {
   H2S_OPT_FAST_PATH = 1,       /* 1 (default): the tile kernel where it applies; 0: generic kernel only */
   H2S_OPT_TILES_PER_BLOCK = 2, /* tile kernel: 64x32 tiles one block walks (1..64, default 8)          */
-  H2S_OPT_HOST_SERIAL = 3      /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
+  H2S_OPT_HOST_SERIAL = 3,     /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
+  H2S_OPT_FAIL_AFTER_LAUNCH = 4 /* test hook: 1 = the next h2s_process call reports H2S_E_HIP right after
+                                   queueing its kernels (the error exits must still record the launch) */
 };
 
 /* Kernel path h2s_process takes for a given frame pair (h2s_query_path). */

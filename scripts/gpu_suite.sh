@@ -9,8 +9,9 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
 export H2S_FLOAT_REPORT=$OUT/float_report.jsonl
+export H2S_PARITY_REPORT=$OUT/parity_report.jsonl   # exact / one-step / beyond shares per integer check
 # (H2S_FLOOR_ONLY_MAX, when set, overrides the per-kind floor-only bounds)
-rm -f "$H2S_FLOAT_REPORT"
+rm -f "$H2S_FLOAT_REPORT" "$H2S_PARITY_REPORT"
 timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_STOP:--x} -q --timeout 300 --timeout-method thread "$@" \
   > "$OUT/pytest_gpu.log" 2>&1
 rc=$?

@@ -74,3 +74,20 @@ def ipt_floor(params, lin, want, floor1):
     dl = dq + d_i[None]
     dlms = _eotf(lp + dl) - _eotf(np.maximum(lp - dl, 0.0))
     return np.einsum('ck,khw->chw', np.abs(l2r), dlms) * 1e4 / tw
+
+
+def pq_eotf_kappa(lin, npl):
+    """Condition number |d ln EOTF / d ln E| of the ST 2084 EOTF at the code
+    value E that produced each linear value lin (units of npl):
+    (1/m1)(1/m2) [xp / (xp - c1) + c3 xp / (c2 - c3 xp)], xp = E^(1/m2).  It
+    grows without bound as E falls to c1^m2 (~7.4e-7, EOTF = 0): there any two
+    float32 evaluations of the same code differ by kappa times the rounding of
+    E itself (about 2^-23 relative), whatever their arithmetic.  0 where lin
+    is 0 (both sides read 0 below the pole)."""
+    m1, m2, c1, c2, c3 = 0.1593017578125, 78.84375, 0.8359375, 18.8515625, 18.6875
+    y = np.nan_to_num(np.abs(lin), nan=0.0, posinf=0.0) * npl / 1e4
+    e = _pq(y)
+    xp = np.clip(e, 0.0, None) ** (1 / m2)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        k = (1 / m1) * (1 / m2) * (xp / (xp - c1) + c3 * xp / (c2 - c3 * xp))
+    return np.where(y > 0, np.nan_to_num(np.abs(k), nan=0.0, posinf=0.0), 0.0)

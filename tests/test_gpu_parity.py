@@ -105,12 +105,14 @@ def parity_report(params, got, want, W, H, q, luma_within=None):
     y_one = float(luma_within.mean()) - y_exact if luma_within is not None else float(((dy > 0) & (dy <= step)).mean())
     c_exact = float((dc == 0).mean())
     c_one = float(((dc > 0) & (dc <= step)).mean())
+    clip = lambda v: max(0.0, v)   # noqa: E731  (float rounding of 1 - a - b)
     rec = dict(test=os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0], pipeline=params.resolved_pipeline(),
                tonemapper=params.tonemapper, bits_in=params.bits_in, bits_out=params.bits_out, gamma=params.gamma,
                W=W, H=H, frames=int(got.shape[0]), quantiser_bits=q,
-               luma=dict(exact=y_exact, one_step=y_one, beyond=1.0 - y_exact - y_one),
-               chroma=dict(exact=c_exact, one_step=c_one, beyond=1.0 - c_exact - c_one),
-               max_diff_steps=int(d.max(initial=0) // step + (d.max(initial=0) % step > 0)))
+               luma=dict(exact=y_exact, one_step=y_one, beyond=clip(1.0 - y_exact - y_one)),
+               chroma=dict(exact=c_exact, one_step=c_one, beyond=clip(1.0 - c_exact - c_one)),
+               # output codes (luma after eq, where one pre-eq step can span several)
+               max_diff_out_steps=int(-(-int(d.max(initial=0)) // step)))
     with open(path, 'a') as fh:
         fh.write(json.dumps(rec) + '\n')
     return rec
@@ -721,6 +723,46 @@ def test_set_params_waits_only_for_its_own_context():
     finally:
         a.close()
         b.close()
+
+
+def test_set_params_waits_for_a_failed_calls_queued_launch():
+    """an h2s_process that fails after queueing its kernels (here
+    the H2S_OPT_FAIL_AFTER_LAUNCH test hook, standing in for a D2H copy or
+    event failure) still records its launch, so the same context's next
+    set_params waits for the queued kernel (queued behind a ~0.3 s spin)
+    before rewriting the tables it reads."""
+    import time
+    import torch
+    from hdr2sdr import _abi
+    W, H = 256, 128
+    p = hdr2sdr.TonemapParams(tonemapper='hable', gamma=2.2)
+    a = hdr2sdr.Tonemapper(0, p, lattice(65))
+    src = synth_frames('smooth', 2, W, H, 10, device='cpu', seed=4).to_torch('cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(2, W, H, 10, 'cuda')
+    a.process(src, dst)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    torch.cuda._sleep(50_000_000)
+    torch.cuda.synchronize()
+    spin = int(50_000_000 * 0.3 / max(time.perf_counter() - t0, 1e-4))
+    try:
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(spin)
+        a.set_option(_abi.OPT_FAIL_AFTER_LAUNCH, 1)
+        with pytest.raises(RuntimeError, match='injected failure'):
+            a.process(src, dst, side)                   # queued behind the spin, then reports an error
+        t0 = time.perf_counter()
+        a.set_params(p.with_(gamma=1.5))
+        ta = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        assert ta > 0.1, f'set_params returned after {ta:.3f} s, before the failed call\'s queued launch ran'
+        a.process(src, dst)                             # the hook fires once: the context works on
+        torch.cuda.synchronize()
+    finally:
+        a.close()
 
 
 def test_two_pass_scratch_serialised_across_streams(tm):

@@ -196,14 +196,17 @@ def test_gpu_preview_batch_mixed_sizes_vs_oracle(tm, use_gpu):
     box = (192, 108)
     with PV.Previewer(0, tonemapper=tm, use_gpu=use_gpu, lattice=_lat()) as pv:
         assert pv.params.peak_detect == (tm == 'bt.2390' or use_gpu)
-        batch = pv.convert_batch(frames, *box, gamma=1.3)
-        singles = [pv.convert(f, *box, gamma=1.3) for f in frames]
+        batch = pv.convert_batch(frames, *box)
+        singles = [pv.convert(f, *box) for f in frames]
+        batch13 = pv.convert_batch(frames, *box, gamma=1.3)
         op = oracle.params_from(pv.params.to_c())
-    for f, (w, h), got, one in zip(frames, sizes, batch, singles):
+    g13 = PV.adjust_gamma_lut(1.3)
+    for f, (w, h), got, one, got13 in zip(frames, sizes, batch, singles, batch13):
         ow, oh = PV.fit_size(w, h, *box)
         assert got.shape == (oh, ow, 3)
         assert np.array_equal(got, one)
-        want = oracle.preview_rgb24(op, _lat(), f.buf, w, h, ow, oh, 1.3)
+        assert np.array_equal(got13, g13[got])          # the display gamma, fused
+        want = oracle.preview_rgb24(op, _lat(), f.buf, w, h, ow, oh, 1.0)
         d = np.abs(got.astype(int) - want.astype(int))
         assert d.max() <= 4 and (d > 1).mean() < 1e-2
 
