@@ -372,6 +372,12 @@ def main():
                           'bits': f"{p_.bits_in}->{p_.bits_out}", 'kernel_ms': round(kms_, 4),
                           'mpx_s': round(nf * w_ * h_ / kms_ / 1e3, 1),
                           'hbm_frac': round(b_ * nf * w_ * h_ / (kms_ / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if p_.resolved_pipeline() == 'libplacebo':
+                # the libplacebo stage is a restatement (no libplacebo in the image):
+                # GPU = oracle is tested, the oracle itself is not pinned to libplacebo;
+                # the detected peak (peak_detect=1) even less so
+                other[tag]['parity'] = ('unpinned: dynamic peak (libplacebo peak_detect restated)'
+                                        if p_.peak_detect else 'unpinned: libplacebo stage restated')
             t_.close()
             del src_, dst_
 

@@ -37,9 +37,9 @@
 //                offset table, one-key uniformity test (9 + 6 half-rate ops -> 6)
 //  H2S_EXPCLAMP  lut3d's [0, N-1] clamp as v_exp_f32's output clamp
 //  H2S_EQMAGIC   eq index by a 2^23 add and a 16-bit shift (full-rate ops)
-//  H2S_DARKEXACT exact EOTF for channels in the PQ table's first segment,
-//                ballot-gated per step (off: +15 % on the website frame,
-//                the per-step branch breaks the straight-line fast body)
+//  H2S_DARKEXACT exact EOTF for channels in the PQ table's first segment
+//                (E' < 1/128, below ~0.0015 nits), ballot-gated per step in
+//                both bodies
 #ifndef H2S_TAGSEL
 #define H2S_TAGSEL 1
 #endif
@@ -132,27 +132,38 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
     static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
     r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
     constexpr float EI = 1.0f / (float)PQ_SEG;
-    // NOEX (the fast body): the tile's codes keep every E inside the table
-    // (tflag) and, with H2S_DARKEXACT, out of its first segment (tdark)
-    if (NOEX) return false;
+    auto dk = [](float u) { return __builtin_bit_cast(unsigned, u) - 0x3F800001u; };
 #if H2S_DARKEXACT
-    // the table's first segment (E < 1/128, staged u < 2: below ~0.0015
+    // the table's first segment (E < 1/128, staged u in (1, 2): below ~0.0015
     // nits) is where EOTF ~ (E - E0)^6.28 and no cubic in t holds 1e-3
-    // relative; a wave with such a channel evaluates those channels exactly
-    // (zimg's formula).  Only tiles whose code ranges allow such a channel
-    // get here (k_tile's tdark bound; about 1 % of the bench content's 8x8
-    // steps hold one)
-    const float emin = __builtin_fminf(__builtin_fminf(er, eg), eb);
-    const bool dark = __builtin_amdgcn_ballot_w64(emin < 2.0f) != 0;
+    // relative; a step with such a channel evaluates those channels exactly
+    // (zimg's formula).  u in (1, 2) <=> u's bit pattern in (0x3F800000,
+    // 0x40000000): bits - 0x3F800001 is below 2^23 - 1 exactly there, and
+    // wraps high for u = 1 (E = 0, black), u < 1 and negative u.  About 1 % of
+    // the bench content's 8x8 steps and 3.6 % of the website frame's hold one
+    // (scripts/dark_step_sim.py)
+    unsigned dmin;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(dmin) : "v"(dk(er)), "v"(dk(eg)), "v"(dk(eb)));
+    const bool dark = __builtin_amdgcn_ballot_w64(dmin < 0x7FFFFFu) != 0;
 #else
     const bool dark = false;
 #endif
+    // NOEX (the fast body): the tile's codes keep every E inside the table
+    // (tflag): no exact path above it, no ballot for it
+    if (NOEX) {
+      if (dark) {
+        r = dk(er) < 0x7FFFFFu ? pq_exact(F, (er - 1.0f) * EI) : r;
+        g = dk(eg) < 0x7FFFFFu ? pq_exact(F, (eg - 1.0f) * EI) : g;
+        b = dk(eb) < 0x7FFFFFu ? pq_exact(F, (eb - 1.0f) * EI) : b;
+      }
+      return false;
+    }
     const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
     const bool high = __builtin_amdgcn_ballot_w64(emax >= PQZ_LIM) != 0;   // rare: extreme out-of-gamut codes
     if (high || dark) {
-      r = er >= PQZ_LIM || er < 2.0f ? pq_exact(F, (er - 1.0f) * EI) : r;
-      g = eg >= PQZ_LIM || eg < 2.0f ? pq_exact(F, (eg - 1.0f) * EI) : g;
-      b = eb >= PQZ_LIM || eb < 2.0f ? pq_exact(F, (eb - 1.0f) * EI) : b;
+      r = er >= PQZ_LIM || (H2S_DARKEXACT && dk(er) < 0x7FFFFFu) ? pq_exact(F, (er - 1.0f) * EI) : r;
+      g = eg >= PQZ_LIM || (H2S_DARKEXACT && dk(eg) < 0x7FFFFFu) ? pq_exact(F, (eg - 1.0f) * EI) : g;
+      b = eb >= PQZ_LIM || (H2S_DARKEXACT && dk(eb) < 0x7FFFFFu) ? pq_exact(F, (eb - 1.0f) * EI) : b;
     }
     return high;
   } else {
@@ -483,6 +494,13 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
 #endif
     }
+    // s is a product when N-1 is not a power of two (N-1 times the clamped
+    // power; 8-bit code / 255 x (N-1) on the libplacebo branch): without this
+    // barrier the compiler contracts the cell origin s - fract(s) below into
+    // fma(N-1, x, -fract(s)), which carries the product's rounding error, so the
+    // origin is no longer an integer and a byte offset truncates to a
+    // misaligned record (N = 177: 45 of 3072 samples of a uniform frame)
+    asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
     const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
     const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * 12.0f));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
@@ -751,22 +769,6 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
   return r;
 }
 
-// smallest / largest of the 8 u16 codes packed in a 16-byte chunk
-__device__ __forceinline__ unsigned min8_u16(uint4 a) {
-  unsigned m, n, o;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(a.x), "v"(a.y));
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(n) : "v"(a.z), "v"(a.w));
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(o) : "v"(m), "v"(n));
-  return min(o & 0xFFFFu, o >> 16);
-}
-__device__ __forceinline__ unsigned max8_u16(uint4 a) {
-  unsigned m, n, o;
-  asm("v_pk_max_u16 %0, %1, %2" : "=v"(m) : "v"(a.x), "v"(a.y));
-  asm("v_pk_max_u16 %0, %1, %2" : "=v"(n) : "v"(a.z), "v"(a.w));
-  asm("v_pk_max_u16 %0, %1, %2" : "=v"(o) : "v"(m), "v"(n));
-  return max(o & 0xFFFFu, o >> 16);
-}
-
 // staging and store helpers of k_tile
 // 8 luma samples -> Y*ys + y_off floats at (row, 8 col8)
 // returns the largest staged value
@@ -890,7 +892,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
-  __shared__ int tdark[2][5];                  // per tile parity: min luma, min/max U, min/max V codes (H2S_DARKEXACT)
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -923,7 +924,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
-  if (t < 10) tdark[t / 5][t % 5] = (t % 5) == 2 || (t % 5) == 4 ? 0 : 0x7FFFFFFF;
   if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
   __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
@@ -1025,17 +1025,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     if ((t & 127) < 72) mc = stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
     const int par = (int)(tile & 1u);
     if ((my > F.safe_y || mc > F.safe_c)) tflag[par] = 1;
-    if (H2S_DARKEXACT && TRC == 0) {
-      // the tile's smallest luma and the range of each chroma plane (raw
-      // codes), for the bound that keeps dark channels out of the fast body
-      atomicMin(&tdark[par][0], (int)min8_u16(cur.ya));
-      if ((t & 127) < 72) {
-        const int pc = (t >> 7) & 1;
-        const unsigned h = cur.uh;
-        atomicMin(&tdark[par][1 + 2 * pc], (int)min(min8_u16(cur.ua), h));
-        atomicMax(&tdark[par][2 + 2 * pc], (int)max(max8_u16(cur.ua), h));
-      }
-    }
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
@@ -1043,22 +1032,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
       cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
     __syncthreads();
-    bool fb = __builtin_amdgcn_readfirstlane(tflag[par]) == 0 && !F.chr444;
+    const bool fb = __builtin_amdgcn_readfirstlane(tflag[par]) == 0 && !F.chr444;
     if (t == 0) tflag[par ^ 1] = 0;   // for the next tile: read by every wave of the previous one before this barrier
-    if (H2S_DARKEXACT && TRC == 0) {
-      // lower bound of every pixel's E (staged units) over the tile: E_c =
-      // Y' + the channel's chroma terms, each at its extreme; a bound below
-      // the table's first segment sends the tile to the checked body
-      const float ymn = (float)__builtin_amdgcn_readfirstlane(tdark[par][0]) * ysc + yoff;
-      const float ulo = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][1]) - cmid);
-      const float uhi = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][2]) - cmid);
-      const float vlo = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][3]) - cmid);
-      const float vhi = 8.0f * ((float)__builtin_amdgcn_readfirstlane(tdark[par][4]) - cmid);
-      const float elo = __builtin_fminf(__builtin_fminf(fmaf(a_rv, vlo, ymn), fmaf(a_bu, ulo, ymn)),
-                                        fmaf(a_gv, vhi, fmaf(a_gu, uhi, ymn)));   // a_rv, a_bu > 0 > a_gu, a_gv
-      fb = fb && !(elo < 2.0f);
-      if (t < 5) tdark[par ^ 1][t] = t == 2 || t == 4 ? 0 : 0x7FFFFFFF;
-    }
     if (fb)
       steps(g, std::integral_constant<bool, true>{});
     else
