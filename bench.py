@@ -42,7 +42,7 @@ def parse_args():
                     help='frames per rank per step (C4: 512 frames / 8 GPUs = 64)')
     ap.add_argument('--width', type=int, default=3840)
     ap.add_argument('--height', type=int, default=2160)
-    ap.add_argument('--kind', default='smooth', help='synthetic content (smooth|uniform|ramp|edges)')
+    ap.add_argument('--kind', default='smooth', help='synthetic content (smooth|uniform|ramp|edges), or website (the reference frame)')
     ap.add_argument('--tonemapper', default='hable')
     ap.add_argument('--gamma', type=float, default=2.2)
     ap.add_argument('--bits-in', type=int, default=10)
@@ -282,7 +282,15 @@ def main():
         del src, dst
         return el, kms, px, cks
 
-    el, kms, px_total, checksum = run(args.kind)
+    real_npz = os.path.join(REPO, 'tests', 'golden', 'website_hdr_full.npz')
+    if args.kind == 'website':   # profiling runs on the reference's own frame (4K only)
+        import numpy as np
+        from hdr2sdr.synth import frames_from_rgb8
+        rgb8w = np.load(real_npz)['hdr']
+        el, kms, px_total, checksum = run('website', lambda n: frames_from_rgb8(rgb8w, n, args.bits_in, dev))
+        del rgb8w
+    else:
+        el, kms, px_total, checksum = run(args.kind)
     alt = None
     if not args.no_alt:
         el_u, kms_u, px_u, _ = run('uniform')
@@ -291,7 +299,6 @@ def main():
     # real content: the reference's own website HDR frame (a 4K capture of PQ
     # BT.2020 R'G'B', tests/golden/website_hdr_full.npz), repeated per frame
     real = None
-    real_npz = os.path.join(REPO, 'tests', 'golden', 'website_hdr_full.npz')
     if world == 1 and not args.no_alt and os.path.exists(real_npz) and (W, H) == (3840, 2160):
         import numpy as np
         from hdr2sdr.synth import frames_from_rgb8
@@ -306,7 +313,8 @@ def main():
     # pipes see.  Reported beside, never as, the headline value.
     host_path = None
     if world == 1 and not args.no_alt:
-        hs = synth_frames(args.kind, B, W, H, args.bits_in, device='cpu', seed=0x5EED).to_numpy()
+        hs = synth_frames('smooth' if args.kind == 'website' else args.kind, B, W, H, args.bits_in, device='cpu',
+                          seed=0x5EED).to_numpy()
         hsrc = hdr2sdr.FrameBatch.empty_pinned(B, W, H, args.bits_in)
         hsrc.buf[...] = hs.buf
         hdst = hdr2sdr.FrameBatch.empty_pinned(B, W, H, args.bits_out)

@@ -632,7 +632,13 @@ constexpr int HST = 68;            // LDS row stride of the horizontally upsampl
 // bypass the L1 (sc1 nt, sc0 sc1 nt) or use workgroup scope (sc0 nt) time the
 // same within 1 %: the streamed bytes do not evict the lattice lines the
 // gathers wait on (profiles/r03/ablations/frame_load_cache_policy.log)
-constexpr int NT = 2;
+#ifndef H2S_NT_LOAD
+#define H2S_NT_LOAD 2
+#endif
+#ifndef H2S_NT_STORE
+#define H2S_NT_STORE 2
+#endif
+constexpr int NT = H2S_NT_LOAD, NTS = H2S_NT_STORE;   // cache-policy bits (ablation builds override)
 
 __device__ __forceinline__ float quad_sum(float v) {
   // (v0 + v1) + (v2 + v3) over the 2x2 pixels of a quad, in all 4 lanes
@@ -817,9 +823,9 @@ __device__ __forceinline__ void put_luma(const FastParams& F, const TileGeo& g, 
   const __amdgpu_buffer_rsrc_t oy_ = plane_rsrc(F.out[0] + g.f * F.out_fp[0], F.out_bytes[0]);
   so += g.py0 * (int)F.out_ls[0];
   if (F.out8)
-    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oy_, vo, so + g.px0, NT);
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oy_, vo, so + g.px0, NTS);
   else
-    __builtin_amdgcn_raw_buffer_store_b128(v, oy_, vo, so + 2 * g.px0, NT);
+    __builtin_amdgcn_raw_buffer_store_b128(v, oy_, vo, so + 2 * g.px0, NTS);
 }
 // chroma plane pl, row r, chunk c (8 samples): ((c0 + c1) + (c2 + c3)) + bias,
 // quantised once per sample, packed as read_luma
@@ -852,9 +858,9 @@ __device__ __forceinline__ void put_chroma(const FastParams& F, const TileGeo& g
   const __amdgpu_buffer_rsrc_t oc_ = plane_rsrc(F.out[1 + pl] + g.f * F.out_fp[1 + pl], F.out_bytes[1 + pl]);
   const int so = g.cy0 * (int)F.out_ls[1 + pl];
   if (F.out8)
-    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oc_, vo, so + g.cx0, NT);
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, oc_, vo, so + g.cx0, NTS);
   else
-    __builtin_amdgcn_raw_buffer_store_b128(v, oc_, vo, so + 2 * g.cx0, NT);
+    __builtin_amdgcn_raw_buffer_store_b128(v, oc_, vo, so + 2 * g.cx0, NTS);
 }
 
 // Each block walks F.tpb consecutive tiles (XCD-remapped, so neighbouring

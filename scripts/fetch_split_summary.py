@@ -23,12 +23,15 @@ for d in sorted(glob.glob(os.path.join(out, '*_lut*_*SIZE'))):
     if vals:
         vals.sort()
         rows[tag] = vals[len(vals) // 2] * 1024   # median dispatch, KiB -> B
-for cfg in ('c2', 'c3', 'c3cpu', 'c3max', 'c3hable'):
-    f65, f2 = rows.get(f'{cfg}_lut65_FETCH_SIZE'), rows.get(f'{cfg}_lut2_FETCH_SIZE')
-    w65 = rows.get(f'{cfg}_lut65_WRITE_SIZE')
+libs = sorted({t.split('.')[0] for t in rows if '.' in t}) or ['']
+for lib in libs:
+  pre = f'{lib}.' if lib else ''
+  for cfg in ('c2', 'c3', 'c3cpu', 'c3max', 'c3hable', 'c2web', 'c3web'):
+    f65, f2 = rows.get(f'{pre}{cfg}_lut65_FETCH_SIZE'), rows.get(f'{pre}{cfg}_lut2_FETCH_SIZE')
+    w65 = rows.get(f'{pre}{cfg}_lut65_WRITE_SIZE')
     if f65 is None or f2 is None:
         continue
     w65 = w65 or 0.0
-    print(f'{cfg}: FETCH raw 65^3 {f65:.4g} B, 2^3 {f2:.4g} B, lattice-induced {f65 - f2:.4g} B raw '
+    print(f'{pre}{cfg}: FETCH raw 65^3 {f65:.4g} B, 2^3 {f2:.4g} B, lattice-induced {f65 - f2:.4g} B raw '
           f'({(f65 - f2) / B_ALG_IN:.3f} x input); x2-corrected totals {2 * f65:.4g} / {2 * f2:.4g} '
           f'(input {B_ALG_IN:.4g}); WRITE {w65:.4g} B')

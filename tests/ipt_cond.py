@@ -55,8 +55,8 @@ def _eotf(e):
 
 
 def ipt_floor(params, lin, want, floor1):
-    """The stage-1 absolute floor (floor1, units of npl: the EOTF table's error
-    next to black) carried through the IPT form to stage 2 (units of the target
+    """The stage-1 absolute uncertainty (floor1, units of npl: a scalar floor,
+    or per channel and pixel as stage1_uncertainty gives it) carried through the IPT form to stage 2 (units of the target
     white).  The PQ re-encode of the LMS rows is unboundedly steep at 0, so a
     channel that is nearly black on input can move its L', M' or S' a lot;
     bounded by secants: dq = PQ(y + dy) - PQ(y - dy), the intensity's share
@@ -67,7 +67,10 @@ def ipt_floor(params, lin, want, floor1):
     tw = 203.0 if params.target_white != params.target_white else params.target_white
     lin = np.nan_to_num(lin)
     y = np.einsum('kc,chw->khw', r2l, lin) * npl / 1e4
-    dy = (np.abs(r2l).sum(1) * floor1 * npl / 1e4)[:, None, None]
+    if np.ndim(floor1) == 0:
+        dy = (np.abs(r2l).sum(1) * floor1 * npl / 1e4)[:, None, None]
+    else:   # per channel and pixel (stage1_uncertainty)
+        dy = np.einsum('kc,chw->khw', np.abs(r2l), floor1) * npl / 1e4
     dq = _pq(y + dy) - _pq(np.maximum(y - dy, 0.0))
     d_i = 2.0 * (0.4 * dq[0] + 0.4 * dq[1] + 0.2 * dq[2])
     lp = _pq(np.maximum(np.einsum('kc,chw->khw', r2l, np.nan_to_num(want)) * tw / 1e4, 0.0))
@@ -91,3 +94,24 @@ def pq_eotf_kappa(lin, npl):
     with np.errstate(divide='ignore', invalid='ignore'):
         k = (1 / m1) * (1 / m2) * (xp / (xp - c1) + c3 * xp / (c2 - c3 * xp))
     return np.where(y > 0, np.nan_to_num(np.abs(k), nan=0.0, posinf=0.0), 0.0)
+
+
+def stage1_uncertainty(lin, npl, transfer):
+    """Absolute stage-1 uncertainty (units of npl, per channel and pixel)
+    that conditioning alone puts between any two float32 evaluations of the
+    EOTF of the same code, with no floor: the PQ EOTF's kappa times the
+    relative disagreement of its inputs -- E itself, a sum of O(1) float32
+    terms (Y' and the chroma products: 2^-22 absolute between two
+    evaluations, so 2^-22 / E relative, large where the terms cancel to a
+    near-black channel), and E^(1/m2), whose 2-ulp disagreement (2^-22)
+    enters the EOTF m2-fold through kappa.  HLG (transfer 'arib-std-b67'):
+    the inverse OETF is well conditioned, 2^-22 relative."""
+    a = np.nan_to_num(np.abs(lin), nan=0.0, posinf=0.0)
+    if transfer not in ('smpte2084', 'pq'):
+        return a * 2.0 ** -22
+    m2 = 78.84375
+    kap = pq_eotf_kappa(lin, npl)
+    e = _pq(a * npl / 1e4)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        rel = np.where(e > 0, 2.0 ** -22 / e, 0.0)
+    return kap * (rel + m2 * 2.0 ** -22) * a

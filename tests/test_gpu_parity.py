@@ -141,7 +141,10 @@ def assert_close_int(params, got, want, W, H, max_frac=5e-3, lut_n=65):
         parity_report(params, got, want, W, H, q)
         assert d.max(initial=0) <= bound, f'max diff {d.max()} > {bound} ({k8} 8-bit R\'G\'B\' steps)'
         frac = float((d > step).mean())
-        assert frac <= max_frac, f'{frac:.3%} of samples beyond one step'
+        # measured (round 4, every libplacebo check of the suite): <= 0.27 %
+        # beyond one step (profiles/r04/parity_report.jsonl); the budget is 0.3 %
+        lp_frac = min(max_frac, 3e-3)
+        assert frac <= lp_frac, f'{frac:.3%} of samples beyond one step (budget {lp_frac:.2%})'
         return
     shift = params.bits_out - q if params.bits_out >= q else 0
     step = 1 << shift
@@ -272,6 +275,7 @@ def test_lut_sizes(tm, lut_n):
 #   stage 3/4 (gamma-encoded / post-LUT R'G'B'): 3.2e-4 at most in gamma space
 #     through x^(1/2.4) near black, and the LUT's slopes up to ~1.7: 6e-4;
 #   stage 5 (quantiser inputs, code units at depth q): 219 * 2^(q-8) * 3e-4.
+TILE_DARK_EXACT = False  # k_tile's PQ first segment exact (h2s_tile.h H2S_DARKEXACT; off in the product)
 EPS_IPT = 1e-4     # LMS relative error of the IPT form on the tile kernel (tests/diag/diag_ipt.py: <= 5.6e-5)
 FLOAT_CFGS = {
     'C2_hable_pq10': dict(tonemapper='hable', gamma=2.2, bits_out=10),
@@ -322,16 +326,21 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     if stage == 3 and kernel == 'k_tile':
         want = np.clip(want, 0.0, 1.0)      # k_tile clamps x to [0, 1) before the power (lattice coordinate)
     q = oracle.quant_bits(op)
-    # The 6e-4 floor on stages 3/4 belongs to k_tile's PQ EOTF table (its first
-    # segment); the generic kernel evaluates the EOTF with powf and keeps the
-    # round-1 floor of 1e-5 on every stage (stage 5 in code units at depth q:
-    # through the Y'CbCr rows, 224 codes per unit at 8 bits).  At stages 4/5
-    # the lattice's slope multiplies the stage-3 disagreement: that term is
-    # carried as conditioning (lattice_slope below), not as a floor.
-    if kernel == 'k_tile':
-        floor = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
-    else:
-        floor = {1: 2e-7, 2: 2e-7, 3: 1e-5, 4: 1e-5, 5: 224 * (1 << (q - 8)) * 1e-5}[stage]
+    # Floors: none at stages 1/2 -- the EOTF's own conditioning (kappa times
+    # the disagreement of its inputs, stage1_uncertainty) is the only
+    # allowance beyond 1e-3 relative; 1e-5 at stages 3/4 and 224 2^(q-8) 1e-5
+    # at stage 5 (code units at depth q).  At stages 4/5 the lattice's slope
+    # multiplies the stage-3 disagreement: carried as conditioning
+    # (lattice_slope below), not as a floor.  The one exception is k_tile's
+    # PQ table's first segment (E < 1/128, below 0.0015 nits), where its cubic
+    # holds 7.3e-8 x npl absolute, not 1e-3 relative: values whose input has
+    # a channel there keep the table's floors (2e-7; through x^(1/2.4) and the
+    # lattice 6e-4; stage 5 219 2^(q-8) 3e-4), and only they.  The exact path
+    # for that segment exists (h2s_tile.h H2S_DARKEXACT) but costs 2.6-4 % on
+    # C2 and 7 % on C3 (profiles/r04/ablations/dark_exact_*.log); with a build
+    # that has it, set TILE_DARK_EXACT and no value keeps a floor
+    floor = {1: 0.0, 2: 0.0, 3: 1e-5, 4: 1e-5, 5: 224 * (1 << (q - 8)) * 1e-5}[stage]
+    floor_seg0 = {1: 2e-7, 2: 2e-7, 3: 6e-4, 4: 6e-4, 5: 219 * (1 << (q - 8)) * 3e-4}[stage]
     got = got.astype(np.float64)
     with np.errstate(invalid='ignore'):
         err = np.abs(got - want)
@@ -351,6 +360,14 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     #   are excluded and counted.
     lin = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 1).astype(np.float64)
     skip = ~(np.nanmax(np.abs(np.nan_to_num(lin, nan=np.inf)), axis=0) < 1e6)
+    from ipt_cond import stage1_uncertainty
+    u1 = stage1_uncertainty(lin, params.npl, params.transfer)
+    if kernel == 'k_tile' and not TILE_DARK_EXACT and params.transfer in ('smpte2084', 'pq'):
+        # k_tile's PQ first segment: per value at stage 1, per pixel after
+        seg0 = (lin > 0) & (lin < oracle.pq_eotf(1.0 / 128) * 1e4 / params.npl)
+        floor = np.where(seg0 if stage == 1 else seg0.any(axis=0)[None], floor_seg0, floor)
+    with np.errstate(invalid='ignore', divide='ignore'):
+        r1 = np.nan_to_num(u1 / np.abs(lin), nan=0.0, posinf=0.0).max(axis=0)   # largest relative, per pixel
     kappa = np.zeros(skip.shape)
     sens = np.ones(want.shape)     # |d stage-2 value / d stage-1 value| for the floor
     if stage >= 2 and params.desat > 0 and params.tonemapper not in ('bt.2390', 'spline'):
@@ -381,7 +398,16 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens
     rel = (1e-3 + 4e-5 * kappa[None]) * np.abs(want)
     tol = rel + floor
-    if kernel != 'k_tile' and stage in (4, 5) and params.lut_enabled and params.resolved_pipeline() != 'libplacebo':
+    # the stage-1 conditioning term, carried: absolute at stage 1; relative
+    # through the tone gain (x2: the gain itself reads the largest channel)
+    # and through x^(1/2.4) (/2.4)
+    if stage == 1:
+        tol = tol + u1
+    elif stage == 2:
+        tol = tol + 2.0 * r1[None] * np.abs(want) * sens
+    elif stage == 3:
+        tol = tol + (2.0 / 2.4) * r1[None] * np.abs(want)
+    if stage in (4, 5) and params.lut_enabled and params.resolved_pipeline() != 'libplacebo':
         # The PQ pow in float32 disagrees by up to ~4e-5 relative between any
         # two implementations (stage 1, see kappa above); x^(1/2.4) divides a
         # relative error by 2.4 and desaturation above its threshold amplifies
@@ -391,7 +417,7 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         # bend next to black (round 2: 1.75e-4 absolute at R'G'B' 0.031 on
         # C4 native 'ramp'), where a floor of 3e-4 used to stand in for it.
         s3 = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 3).astype(np.float64)
-        d3 = (4e-5 / 2.4) * (1.0 + kappa[None]) * np.abs(np.nan_to_num(s3)) + 1e-5
+        d3 = ((4e-5 * (1.0 + kappa[None]) + 2.0 * r1[None]) / 2.4) * np.abs(np.nan_to_num(s3)) + 1e-5
         cond4 = np.einsum('cahw,ahw->chw', lattice_slope(65, s3), d3)
         if stage == 5:
             cond4 = 224 * (1 << (q - 8)) * cond4.max(axis=0, keepdims=True)
@@ -406,7 +432,9 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         # the PQ re-encode of a nearly black LMS row is steep (ipt_floor)
         from ipt_cond import ipt_channel_scale, ipt_floor, lp_encode_spread
         w2 = want if stage == 2 else oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 2).astype(np.float64)
-        d2 = EPS_IPT * ipt_channel_scale(w2) + ipt_floor(params, lin, w2, 2e-7)
+        f1 = u1 + (np.where(seg0, 2e-7, 0.0) if kernel == 'k_tile' and not TILE_DARK_EXACT
+                   and params.transfer in ('smpte2084', 'pq') else 0.0)
+        d2 = EPS_IPT * ipt_channel_scale(w2) + ipt_floor(params, lin, w2, f1)
         if stage == 3 and not params.lut_enabled:      # LUT off: the BT.2020 -> 709 matrix first
             m709 = np.array(oracle.BT2020_TO_BT709)
             w2, d2 = np.einsum('ck,khw->chw', m709, np.nan_to_num(w2)), np.einsum('ck,khw->chw', np.abs(m709), d2)
