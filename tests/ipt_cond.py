@@ -105,10 +105,21 @@ def stage1_uncertainty(lin, npl, transfer):
     evaluations, so 2^-22 / E relative, large where the terms cancel to a
     near-black channel), and E^(1/m2), whose 2-ulp disagreement (2^-22)
     enters the EOTF m2-fold through kappa.  HLG (transfer 'arib-std-b67'):
-    the inverse OETF is well conditioned, 2^-22 relative."""
+    below E = 1/2 the inverse OETF is E^2 / 3 and the OOTF raises it to 1.2,
+    so the same 2^-22 absolute in E is 2.4 x 2^-22 / E relative, E estimated
+    back from the display value (1000-nit peak)."""
     a = np.nan_to_num(np.abs(lin), nan=0.0, posinf=0.0)
     if transfer not in ('smpte2084', 'pq'):
-        return a * 2.0 ** -22
+        # display -> scene light per channel: Fd = 1000 Ys^0.2 Fs (units of
+        # nits), Ys the scene luminance (BT.2100 OOTF)
+        yd = np.einsum('c,chw->hw', np.array([0.2627, 0.6780, 0.0593]), a) * npl / 1000.0
+        ys = yd ** (1 / 1.2)
+        with np.errstate(divide='ignore', invalid='ignore'):
+            fs = np.where(ys > 0, a * npl / 1000.0 / ys[None] ** 0.2, 0.0)
+        e = np.sqrt(3.0 * np.minimum(fs, 1.0 / 12))          # the square-law branch
+        with np.errstate(divide='ignore', invalid='ignore'):
+            rel = np.where(e > 0, 2.4 * 2.0 ** -22 / e, 0.0)
+        return (rel + 2.0 ** -22) * a
     m2 = 78.84375
     kap = pq_eotf_kappa(lin, npl)
     e = _pq(a * npl / 1e4)

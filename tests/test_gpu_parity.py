@@ -304,6 +304,27 @@ FLOAT_CFGS = {
 FLOOR_ONLY_MAX = {'ramp': 0.06, 'edges': 0.05, 'uniform': 0.03, 'smooth': 0.02}
 
 
+def tone_uncertainty(params, op):
+    """Absolute stage-2 uncertainty (units of the curve's output white) of a
+    tone curve whose float32 form cancels next to black: Hable's
+    (x(Ax+CB)+DE)/(x(Ax+B)+DF) - E/F subtracts two values near E/F = 0.067,
+    so any two float32 evaluations differ by a few ulp of E/F, 2^-21 E/F,
+    divided by the normalisation hable(peak) -- 2 % of a 4e-7 output.  Both
+    vf_tonemap's form and libplacebo's (NORM scaling: the source peak over the
+    SDR white) have it; 0 for the other curves."""
+    if params.tonemapper != 'hable':
+        return 0.0
+    A, B, C, D, E, F = 0.15, 0.50, 0.10, 0.20, 0.02, 0.30
+
+    def hable(x):
+        return (x * (A * x + C * B) + D * E) / (x * (A * x + B) + D * F) - E / F
+    if params.resolved_pipeline() == 'libplacebo':
+        peak = oracle.resolved(op)[0] * params.npl / 203.0    # source peak over the SDR white (lp NORM)
+    else:
+        peak = oracle.resolved(op)[0]
+    return 2.0 ** -21 * (E / F) / hable(max(peak, 1.0))
+
+
 def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     """One (kernel, config, content, stage) float check; returns its report."""
     import json
@@ -364,7 +385,9 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     u1 = stage1_uncertainty(lin, params.npl, params.transfer)
     if kernel == 'k_tile' and not TILE_DARK_EXACT and params.transfer in ('smpte2084', 'pq'):
         # k_tile's PQ first segment: per value at stage 1, per pixel after
-        seg0 = (lin > 0) & (lin < oracle.pq_eotf(1.0 / 128) * 1e4 / params.npl)
+        # (E at or below the EOTF's zero included: the table's cubic is not
+        # exactly 0 there where the oracle is)
+        seg0 = np.nan_to_num(lin, nan=np.inf) < oracle.pq_eotf(1.0 / 128) * 1e4 / params.npl
         floor = np.where(seg0 if stage == 1 else seg0.any(axis=0)[None], floor_seg0, floor)
     with np.errstate(invalid='ignore', divide='ignore'):
         r1 = np.nan_to_num(u1 / np.abs(lin), nan=0.0, posinf=0.0).max(axis=0)   # largest relative, per pixel
@@ -395,18 +418,29 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         with np.errstate(invalid='ignore', divide='ignore'), warnings.catch_warnings():
             warnings.simplefilter('ignore', RuntimeWarning)     # all-NaN pixels ('edges' codes)
             gain = np.nanmax(np.abs(want), axis=0) / np.nanmax(np.abs(lin), axis=0)
-        floor = floor * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens
+        # the pixel's stage-1 uncertainty, carried as round 3 carried its floor:
+        # by the tone gain and the below-threshold desaturation's sensitivity
+        floor = (floor + u1.max(axis=0)[None]) * np.maximum(1.0, np.nan_to_num(gain, nan=1.0, posinf=1.0))[None] * sens \
+            + tone_uncertainty(params, op)
     rel = (1e-3 + 4e-5 * kappa[None]) * np.abs(want)
     tol = rel + floor
-    # the stage-1 conditioning term, carried: absolute at stage 1; relative
-    # through the tone gain (x2: the gain itself reads the largest channel)
-    # and through x^(1/2.4) (/2.4)
+    # the stage-1 conditioning term, carried: absolute at stage 1 (and, above,
+    # at stage 2 through the gain); relative through x^(1/2.4) (/2.4, x2: the
+    # gain itself reads the largest channel)
     if stage == 1:
         tol = tol + u1
-    elif stage == 2:
-        tol = tol + 2.0 * r1[None] * np.abs(want) * sens
-    elif stage == 3:
-        tol = tol + (2.0 / 2.4) * r1[None] * np.abs(want)
+    if stage >= 3:
+        # the tone curve's own cancellation (tone_uncertainty) as a relative
+        # error of the stage-2 value, through x^(1/2.4)
+        ut = tone_uncertainty(params, op)
+        if ut > 0:
+            w2t = np.abs(np.nan_to_num(oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 2).astype(np.float64)))
+            with np.errstate(divide='ignore', invalid='ignore'):
+                r2 = np.nan_to_num(ut / w2t, nan=0.0, posinf=0.0)
+        else:
+            r2 = np.zeros(want.shape)
+    if stage == 3:
+        tol = tol + ((2.0 * r1[None] + r2) / 2.4) * np.abs(want)
     if stage in (4, 5) and params.lut_enabled and params.resolved_pipeline() != 'libplacebo':
         # The PQ pow in float32 disagrees by up to ~4e-5 relative between any
         # two implementations (stage 1, see kappa above); x^(1/2.4) divides a
@@ -417,7 +451,7 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         # bend next to black (round 2: 1.75e-4 absolute at R'G'B' 0.031 on
         # C4 native 'ramp'), where a floor of 3e-4 used to stand in for it.
         s3 = oracle.debug_float(op, lattice(65), src.to_numpy().buf, W, H, 3).astype(np.float64)
-        d3 = ((4e-5 * (1.0 + kappa[None]) + 2.0 * r1[None]) / 2.4) * np.abs(np.nan_to_num(s3)) + 1e-5
+        d3 = ((4e-5 * (1.0 + kappa[None]) + 2.0 * r1[None] + r2) / 2.4) * np.abs(np.nan_to_num(s3)) + 1e-5
         cond4 = np.einsum('cahw,ahw->chw', lattice_slope(65, s3), d3)
         if stage == 5:
             cond4 = 224 * (1 << (q - 8)) * cond4.max(axis=0, keepdims=True)
@@ -442,13 +476,18 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
     # what the assertion actually rests on, over the kept values
     with np.errstate(invalid='ignore', divide='ignore'):
         beyond_rel = keep & (err > rel)                        # would fail 1e-3 (+ kappa term) alone
-        floor_only = beyond_rel & (err <= tol)                 # ... and pass through a floor / conditioning term
+        # values within 1e-3 of the floor of zero have no relative scale (the
+        # chroma of a neutral pixel at stage 5, E at the EOTF's zero): counted
+        # apart, not as floor use
+        near_zero = keep & (np.abs(want) < 1e-3 * np.broadcast_to(floor, want.shape))
+        floor_only = beyond_rel & (err <= tol) & ~near_zero    # ... and pass through a floor / conditioning term
         # (for the generic kernel's stages 4/5 that share includes the lattice-slope term)
         relerr = np.where(keep & ~beyond_rel & (np.abs(want) > 0), err / np.abs(want), 0.0)
     report = dict(kernel=kernel, cfg=cfg, kind=kind, stage=stage, values=int(want.size),
                   excluded_px=int(skip.sum()), excluded_frac=float(skip.mean()),
                   floor_set_frac=float((keep & (np.broadcast_to(floor, want.shape) > rel)).sum() / max(1, keep.sum())),
                   floor_only_frac=float(floor_only.sum() / max(1, keep.sum())),
+                  near_zero_frac=float((beyond_rel & near_zero).sum() / max(1, keep.sum())),
                   max_rel_err_rest=float(relerr.max(initial=0.0)))
     if os.environ.get('H2S_FLOAT_REPORT'):
         with open(os.environ['H2S_FLOAT_REPORT'], 'a') as fh:
@@ -466,6 +505,12 @@ def check_float_stage(tm, kernel, cfg, kind, stage, W=128, H=64):
         assert (err[keep] <= lim).all(), f'max {float(err[keep].max()):.4g} > {lim:.4g}'
         return report
     bad = (err > tol) & keep
+    if os.environ.get('H2S_FLOAT_DEBUG') and bad.any():   # the worst few, with what their tolerance was made of
+        for i in np.argsort(np.where(bad, err / tol, 0).ravel())[::-1][:4]:
+            c, y, x = np.unravel_index(i, want.shape)
+            print(f'  [{kernel} {cfg} {kind} s{stage}] c{c} ({y},{x}) lin {lin[:, y, x].tolist()} want {want[c, y, x]:.6g} '
+                  f'got {got[c, y, x]:.6g} tol {tol[c, y, x]:.3g} floor {np.broadcast_to(floor, want.shape)[c, y, x]:.3g} '
+                  f'u1 {u1[:, y, x].tolist()} sens {sens[c, y, x]:.3g} kappa {kappa[y, x]:.3g}', flush=True)
     i = int(np.argmax(np.where(bad, err / tol, 0)))
     assert not bad.any(), (f'{kernel} stage {stage}: {int(bad.sum())} values beyond 1e-3 rel + {float(np.max(floor)):g} '
                            f'({int(skip.sum())} ill-conditioned pixels excluded); worst: want '
