@@ -207,7 +207,7 @@ def test_libplacebo_tile_equals_generic(tm, case):
 @pytest.mark.parametrize('kw,min_changed', [
     (dict(lp_range='limited'), 0.5),                          # every code moves towards mid-grey
     (dict(lp_dither='ordered'), 0.02),                        # a fraction of the codes step by one
-    (dict(lp_p010='truncate', bits_in=12), 0.02),             # 12-bit input: two low bits dropped
+    (dict(lp_p010='keep', bits_in=12), 0.02),                 # 12-bit input: two low bits kept (default: dropped)
 ])
 def test_libplacebo_options_change_the_output(tm, kw, min_changed):
     base = hdr2sdr.TonemapParams(tonemapper='bt.2390', bits_in=kw.get('bits_in', 10))
@@ -226,7 +226,7 @@ def test_p010_truncate_has_no_effect_on_10bit_input(tm):
     tm.set_params(p)
     tm.set_lut(lattice(65))
     a = tm(src).to_numpy().buf
-    tm.set_params(p.with_(lp_p010='truncate'))
+    tm.set_params(p.with_(lp_p010='keep' if p.lp_p010 == 'truncate' else 'truncate'))
     assert np.array_equal(tm(src).to_numpy().buf, a)
 
 
