@@ -626,8 +626,14 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
 }
 
 constexpr int CBW = 32, CBH = 16;  // chroma tile
-constexpr int YST = 68;            // LDS row stride (floats) of the luma tile
-constexpr int HST = 68;            // LDS row stride of the horizontally upsampled chroma rows
+#ifndef H2S_YST
+#define H2S_YST 72
+#endif
+// 72 floats: a step's 8 rows x 8 columns then start 8 banks apart and cover
+// all 64 banks (68 overlapped 2-way: 34 % -> 20 % of LDS-active cycles in
+// bank conflicts, time unchanged; profiles/r04/ablations/lds_stride.txt)
+constexpr int YST = H2S_YST;       // LDS row stride (floats) of the luma tile
+constexpr int HST = H2S_YST;       // LDS row stride of the horizontally upsampled chroma rows
 // buffer-op aux bits: non-temporal (streamed frame bytes).  Frame loads that
 // bypass the L1 (sc1 nt, sc0 sc1 nt) or use workgroup scope (sc0 nt) time the
 // same within 1 %: the streamed bytes do not evict the lattice lines the
