@@ -629,11 +629,15 @@ constexpr int CBW = 32, CBH = 16;  // chroma tile
 #ifndef H2S_YST
 #define H2S_YST 72
 #endif
-// 72 floats: a step's 8 rows x 8 columns then start 8 banks apart and cover
-// all 64 banks (68 overlapped 2-way: 34 % -> 20 % of LDS-active cycles in
-// bank conflicts, time unchanged; profiles/r04/ablations/lds_stride.txt)
-constexpr int YST = H2S_YST;       // LDS row stride (floats) of the luma tile
-constexpr int HST = H2S_YST;       // LDS row stride of the horizontally upsampled chroma rows
+// LDS row stride (floats) of the staged luma tile and of the horizontally
+// upsampled chroma rows.  72 on the CPU chain's instances: a step's 8 rows x 8
+// columns then start 8 banks apart and cover all 64 banks (68 overlapped
+// 2-way: 34 % -> 20 % of LDS-active cycles in bank conflicts, time unchanged;
+// profiles/r04/ablations/lds_stride.txt).  68 on the libplacebo instances,
+// whose PQ-encode table and native-depth eq table leave no room: +1.1 KB there
+// drops them from 5 blocks per CU to 4 (C3 +9 %)
+template <int LP>
+constexpr int row_stride() { return LP ? 68 : H2S_YST; }
 // buffer-op aux bits: non-temporal (streamed frame bytes).  Frame loads that
 // bypass the L1 (sc1 nt, sc0 sc1 nt) or use workgroup scope (sc0 nt) time the
 // same within 1 %: the streamed bytes do not evict the lattice lines the
@@ -784,6 +788,7 @@ __device__ __forceinline__ TileRegs tile_load(const FastParams& F, const TileGeo
 // staging and store helpers of k_tile
 // 8 luma samples -> Y*ys + y_off floats at (row, 8 col8)
 // returns the largest staged value
+template <int YST>
 __device__ __forceinline__ float stage_luma(float* yin, uint4 a, int row, int col8, float ysc, float yoff) {
   float v[8];
   unpack8(a, v);
@@ -799,6 +804,7 @@ __device__ __forceinline__ float stage_luma(float* yin, uint4 a, int row, int co
 // h[2k] = 2 c[k], h[2k+1] = c[k] + c[k+1]; exact in float.  tt: chunk index
 // (row tt >> 2, 8-sample chunk tt & 3) of the tile's 18 x 4 chroma chunks
 // returns the largest |centred code|
+template <int HST>
 __device__ __forceinline__ float stage_chroma(float* plane, uint4 a, unsigned h, int tt, float cmid) {
   float v[9];
   unpack8(a, v);
@@ -817,6 +823,7 @@ __device__ __forceinline__ float stage_chroma(float* plane, uint4 a, unsigned h,
 }
 // luma codes of tile row r, chunk c (8 pixels), packed for one 16-byte (u16)
 // / 8-byte (u8: .xy) store
+template <int YST>
 __device__ __forceinline__ u4v read_luma(const FastParams& F, const float* yin, int r, int c) {
   const unsigned* src = reinterpret_cast<const unsigned*>(yin) + r * YST + 8 * c;
   const uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(src + 4);
@@ -896,6 +903,7 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 #define H2S_TILE_WPE 5
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WPE))) void k_tile(const FastParams F) {
+  constexpr int YST = row_stride<LP>(), HST = YST;
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
@@ -1032,9 +1040,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
       mask_in(cur.ya), mask_in(cur.ua);
       cur.uh &= F.in_mask2;
     }
-    const float my = stage_luma(yin, cur.ya, t >> 3, t & 7, ysc, yoff);
+    const float my = stage_luma<YST>(yin, cur.ya, t >> 3, t & 7, ysc, yoff);
     float mc = 0.0f;
-    if ((t & 127) < 72) mc = stage_chroma(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
+    if ((t & 127) < 72) mc = stage_chroma<HST>(hrow[__builtin_amdgcn_readfirstlane(t >> 7)], cur.ua, cur.uh, t & 127, cmid);
     const int par = (int)(tile & 1u);
     if ((my > F.safe_y || mc > F.safe_c)) tflag[par] = 1;
     const TileGeo g = geo;
@@ -1053,7 +1061,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     __syncthreads();
 
     // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----
-    put_luma(F, g, read_luma(F, yin, t >> 3, t & 7), t >> 3, lofs.sy, 0);
+    put_luma(F, g, read_luma<YST>(F, yin, t >> 3, t & 7), t >> 3, lofs.sy, 0);
     if (cst) put_chroma(F, g, read_chroma(F, csum[0], pl, rem >> 2, rem & 3), pl, rem >> 2, lofs.sc);
     if (!more) break;
     ++tile;
