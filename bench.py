@@ -52,6 +52,7 @@ def parse_args():
     ap.add_argument('--mode', default='compat8')
     ap.add_argument('--pipeline', default='auto', help='auto | cpu | libplacebo (profiling runs of one chain)')
     ap.add_argument('--lp-tone', default='ipt', help='libplacebo branch tone form: ipt | max-rgb')
+    ap.add_argument('--peak-detect', action='store_true', help='dynamic peak (profiling runs of C3_dyn)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline budget (0 = skip)')
     ap.add_argument('--no-alt', action='store_true', help='skip the uniform-content secondary run')
     ap.add_argument('--no-sharded', action='store_true',
@@ -242,7 +243,8 @@ def main():
 
     params = hdr2sdr.TonemapParams(tonemapper=args.tonemapper, gamma=args.gamma, bits_in=args.bits_in,
                                    bits_out=args.bits_out, transfer=args.transfer, mode=args.mode,
-                                   pipeline=args.pipeline, lp_tone=args.lp_tone)
+                                   pipeline=args.pipeline, lp_tone=args.lp_tone,
+                                   **(dict(peak_detect=True, maxcll=4000.0) if args.peak_detect else {}))
     # params + LUT lattice: built on rank 0, broadcast over RCCL (frames never move)
     n = args.lut
     lattice_host = hdr2sdr.generate_lattice(n) if rank == 0 else None
