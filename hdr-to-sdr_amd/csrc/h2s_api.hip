@@ -67,7 +67,10 @@ struct h2s_ctx {
   size_t peak_cap = 0;
   h2s::CurveConsts* d_curve = nullptr;    // one curve record per frame of a dynamic-peak launch
   size_t curve_cap = 0;
-  std::vector<h2s::CurveConsts> h_curve;  // host side of the last upload (alive until it completes)
+  h2s::CurveConsts* h_curve = nullptr;    // pinned host side of the last upload (alive until it completes)
+  size_t h_curve_cap = 0;
+  void* h_stats = nullptr;                // pinned landing buffer of the peak statistics (partials + histograms)
+  size_t h_stats_cap = 0;
   hipEvent_t curve_ev = nullptr;          // recorded after the launch that reads d_curve
   double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
   long long pk_frames = 0;
@@ -754,6 +757,8 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_curve) hipFree(c->d_curve);
   if (c->d_chr) hipFree(c->d_chr);
   if (c->d_hist) hipFree(c->d_hist);
+  if (c->h_curve) hipHostFree(c->h_curve);
+  if (c->h_stats) hipHostFree(c->h_stats);
   if (c->curve_ev) hipEventDestroy(c->curve_ev);
   if (c->chr_ev) hipEventDestroy(c->chr_ev);
   for (hipEvent_t ev : c->pend) hipEventDestroy(ev);
@@ -1364,13 +1369,26 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
     }
     c->hist_cap = hneed;
   }
+  // the statistics come back into pinned memory (a pageable destination
+  // costs a staged copy per call on the dynamic-peak path's critical round trip)
+  const size_t sbytes = need * sizeof(float2) + hneed * sizeof(unsigned);
+  if (sbytes > c->h_stats_cap) {
+    if (c->h_stats) hipHostFree(c->h_stats);
+    c->h_stats = nullptr;
+    c->h_stats_cap = 0;
+    if (hipHostMalloc(&c->h_stats, sbytes, hipHostMallocDefault) != hipSuccess) {
+      c->h_stats = nullptr;
+      return fail(c, H2S_E_OOM, "peak statistics host buffer allocation failed");
+    }
+    c->h_stats_cap = sbytes;
+  }
+  const float2* part = static_cast<const float2*>(c->h_stats);
+  const unsigned* hist = reinterpret_cast<const unsigned*>(part + need);
   hipError_t e = pct ? hipMemsetAsync(c->d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
   if (e == hipSuccess) e = h2s::launch_peak_stats(k, c->d_peak, pct ? c->d_hist : nullptr, s);
-  std::vector<float2> part(need);
-  std::vector<unsigned> hist(hneed);
-  if (e == hipSuccess) e = hipMemcpyAsync(part.data(), c->d_peak, need * sizeof(float2), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_stats, c->d_peak, need * sizeof(float2), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && pct)
-    e = hipMemcpyAsync(hist.data(), c->d_hist, hneed * sizeof(unsigned), hipMemcpyDeviceToHost, s);
+    e = hipMemcpyAsync(const_cast<unsigned*>(hist), c->d_hist, hneed * sizeof(unsigned), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
   const double npx = (double)k.W * k.H;
@@ -1383,7 +1401,7 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
       mx = v.x > mx ? v.x : mx;
       sum += v.y;
     }
-    (*fmax)[f] = pct ? pq_percentile(&hist[(size_t)f * h2s::PEAK_BINS], h2s::PEAK_BINS, k.pd_percentile, mx) : mx;
+    (*fmax)[f] = pct ? pq_percentile(hist + (size_t)f * h2s::PEAK_BINS, h2s::PEAK_BINS, k.pd_percentile, mx) : mx;
     (*favg)[f] = sum / npx;
   }
   return 0;
@@ -1397,7 +1415,17 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
   std::vector<KParams> kfs(nframes, k);
   if (fast) {
     if (c->curve_ev && (e = hipEventSynchronize(c->curve_ev)) != hipSuccess) return hip_fail(c, e, "curve upload");
-    c->h_curve.resize(nframes);
+    if ((size_t)nframes > c->h_curve_cap) {
+      if (c->h_curve) hipHostFree(c->h_curve);
+      c->h_curve = nullptr;
+      c->h_curve_cap = 0;
+      if (hipHostMalloc((void**)&c->h_curve, (size_t)nframes * sizeof(h2s::CurveConsts), hipHostMallocDefault) !=
+          hipSuccess) {
+        c->h_curve = nullptr;
+        return fail(c, H2S_E_OOM, "curve records host buffer allocation failed");
+      }
+      c->h_curve_cap = nframes;
+    }
   }
   for (int f = 0; f < nframes; f++) {
     KParams& kf = kfs[f];
@@ -1428,7 +1456,7 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
       c->curve_ev = nullptr;
       return hip_fail(c, e, "curve event");
     }
-    e = hipMemcpyAsync(c->d_curve, c->h_curve.data(), (size_t)nframes * sizeof(h2s::CurveConsts),
+    e = hipMemcpyAsync(c->d_curve, c->h_curve, (size_t)nframes * sizeof(h2s::CurveConsts),
                        hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
     if (e == hipSuccess) e = hipEventRecord(c->curve_ev, s);
