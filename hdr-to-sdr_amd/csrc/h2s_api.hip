@@ -63,14 +63,13 @@ struct h2s_ctx {
   void* d_prev = nullptr;  // preview scratch
   size_t prev_bytes = 0;
   // dynamic peak (params.peak_detect): per-frame stats buffer + IIR state
-  float2* d_peak = nullptr;
-  size_t peak_cap = 0;
+  void* d_stats = nullptr;       // peak statistics: per-block partials, then (percentile model) histograms
+  size_t stats_cap = 0;
   h2s::CurveConsts* d_curve = nullptr;    // one curve record per frame of a dynamic-peak launch
   size_t curve_cap = 0;
   h2s::CurveConsts* h_curve = nullptr;    // pinned host side of the last upload (alive until it completes)
   size_t h_curve_cap = 0;
-  void* h_stats = nullptr;                // pinned landing buffer of the peak statistics (partials + histograms)
-  size_t h_stats_cap = 0;
+  void* h_stats = nullptr;                // pinned landing buffer of d_stats (stats_cap bytes)
   hipEvent_t curve_ev = nullptr;          // recorded after the launch that reads d_curve
   double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
   long long pk_frames = 0;
@@ -94,8 +93,6 @@ struct h2s_ctx {
   hipStream_t aux = nullptr;
   bool chr_pending = false;
   float2* d_chr = nullptr;       // BICUBIC chroma: one frame's per-pixel (Cb, Cr)
-  unsigned* d_hist = nullptr;    // peak_detect percentile: per-frame PQ histograms
-  size_t hist_cap = 0;
   size_t chr_cap = 0;
 };
 
@@ -753,10 +750,9 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_pqi) hipFree(c->d_pqi);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
-  if (c->d_peak) hipFree(c->d_peak);
+  if (c->d_stats) hipFree(c->d_stats);
   if (c->d_curve) hipFree(c->d_curve);
   if (c->d_chr) hipFree(c->d_chr);
-  if (c->d_hist) hipFree(c->d_hist);
   if (c->h_curve) hipHostFree(c->h_curve);
   if (c->h_stats) hipHostFree(c->h_stats);
   if (c->curve_ev) hipEventDestroy(c->curve_ev);
@@ -1346,49 +1342,34 @@ static double pq_percentile(const unsigned* h, int nb, double pct, double mx) {
 static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, std::vector<double>* fmax,
                        std::vector<double>* favg) {
   const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
-  if (need > c->peak_cap) {
-    if (c->d_peak) hipFree(c->d_peak);
-    c->d_peak = nullptr;
-    c->peak_cap = 0;
-    if (hipMalloc((void**)&c->d_peak, need * sizeof(float2)) != hipSuccess) {
-      c->d_peak = nullptr;
-      return fail(c, H2S_E_OOM, "peak statistics allocation failed");
-    }
-    c->peak_cap = need;
-  }
   // pd_percentile < 100: a per-frame histogram of PQ(max R,G,B) as well
   const bool pct = k.pd_percentile < 100.0;
   const size_t hneed = pct ? (size_t)nframes * h2s::PEAK_BINS : 0;
-  if (hneed > c->hist_cap) {
-    if (c->d_hist) hipFree(c->d_hist);
-    c->d_hist = nullptr;
-    c->hist_cap = 0;
-    if (hipMalloc((void**)&c->d_hist, hneed * sizeof(unsigned)) != hipSuccess) {
-      c->d_hist = nullptr;
-      return fail(c, H2S_E_OOM, "peak histogram allocation failed");
-    }
-    c->hist_cap = hneed;
-  }
-  // the statistics come back into pinned memory (a pageable destination
-  // costs a staged copy per call on the dynamic-peak path's critical round trip)
+  // partials and histograms in one device buffer and one pinned host buffer,
+  // so that one copy brings them back (the round trip between the statistics
+  // launch and the tile launch is on every dynamic-peak call's critical path)
   const size_t sbytes = need * sizeof(float2) + hneed * sizeof(unsigned);
-  if (sbytes > c->h_stats_cap) {
+  if (sbytes > c->stats_cap) {
+    if (c->d_stats) hipFree(c->d_stats);
     if (c->h_stats) hipHostFree(c->h_stats);
-    c->h_stats = nullptr;
-    c->h_stats_cap = 0;
-    if (hipHostMalloc(&c->h_stats, sbytes, hipHostMallocDefault) != hipSuccess) {
-      c->h_stats = nullptr;
-      return fail(c, H2S_E_OOM, "peak statistics host buffer allocation failed");
+    c->d_stats = c->h_stats = nullptr;
+    c->stats_cap = 0;
+    if (hipMalloc(&c->d_stats, sbytes) != hipSuccess || hipHostMalloc(&c->h_stats, sbytes, hipHostMallocDefault) != hipSuccess) {
+      if (c->d_stats) hipFree(c->d_stats);
+      c->d_stats = c->h_stats = nullptr;
+      return fail(c, H2S_E_OOM, "peak statistics allocation failed");
     }
-    c->h_stats_cap = sbytes;
+    c->stats_cap = sbytes;
   }
+  float2* d_part = static_cast<float2*>(c->d_stats);
+  unsigned* d_hist = reinterpret_cast<unsigned*>(d_part + need);
   const float2* part = static_cast<const float2*>(c->h_stats);
   const unsigned* hist = reinterpret_cast<const unsigned*>(part + need);
-  hipError_t e = pct ? hipMemsetAsync(c->d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
-  if (e == hipSuccess) e = h2s::launch_peak_stats(k, c->d_peak, pct ? c->d_hist : nullptr, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_stats, c->d_peak, need * sizeof(float2), hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && pct)
-    e = hipMemcpyAsync(const_cast<unsigned*>(hist), c->d_hist, hneed * sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  hipError_t e = pct ? hipMemsetAsync(d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
+  if (e == hipSuccess) e = h2s::launch_peak_stats(k, d_part, pct ? d_hist : nullptr, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_stats, c->d_stats, sbytes, hipMemcpyDeviceToHost, s);
+  // (polling an event instead of this blocking wait measured no better:
+  // profiles/r04/c3_dyn/round_trip_*.txt)
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
   const double npx = (double)k.W * k.H;
