@@ -45,11 +45,12 @@ OBJ_DIR = os.path.join(PROJ_DIR, 'build', 'obj')
 # slots per pixel 207 -> 199)
 CFLAGS = ['-O3', '-std=c++17', '-fno-slp-vectorize', '-fPIC', '-Wno-unused-value', '-Wno-unused-result',
           '-Wno-pass-failed']
-# the product tile kernel: LLVM's max-memory-clause scheduler measured 2 %
-# faster than the default on C2 (smooth / uniform content alike, identical
-# output; profiles/r02/ablations/sched_strategy_v4.log); the higher-occupancy
-# iterative-minreg schedule is 13 % slower
-SOURCE_FLAGS = {'h2s_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-memory-clause']}
+# the product tile kernel's scheduler: round 2 measured LLVM's
+# max-memory-clause 2 % faster than the default; after round 4's changes the
+# default is the faster one (C2 -0.7 % smooth, -3 % uniform noise; Mobius
+# alike; identical output: profiles/r04/ablations/sched_strategy.log), so the
+# tile TU builds with the default again (iterative-minreg stays 13 % slower)
+SOURCE_FLAGS = {}
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:

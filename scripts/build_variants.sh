@@ -13,7 +13,7 @@ O=$ROOT/hdr-to-sdr_amd/build/obj
 V=$ROOT/scripts/variants
 mkdir -p "$V"
 FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed"
-MMC="-mllvm -amdgpu-sched-strategy=max-memory-clause"   # _build.py SOURCE_FLAGS (h2s_fast.hip only)
+MMC=${MMC-""}   # extra flags for h2s_fast.hip (_build.py SOURCE_FLAGS; env MMC overrides)
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
