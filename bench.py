@@ -499,6 +499,19 @@ def main():
         # k_tile's instruction mix from the same PMC passes (per pixel)
         rec['roofline']['instructions_per_px'] = {k: tr[k] for k in ('valu_per_px', 'trans_per_px', 'cvt_per_px',
                                                                       'lds_per_px', 'vmem_rd_per_px') if k in tr}
+        # the unit that actually binds, from the same
+        # PMC passes: VALU wave-instructions per CU-cycle (1.0 = the four
+        # SIMDs' issue peak), texture-data busy share; 'frac' stays the HBM
+        # fraction north_star's roofline asks for
+        for k in ('valu_issue_frac', 'valu_active_frac', 'td_busy_frac'):
+            if k in tr:
+                rec['roofline'][k] = tr[k]
+        if tr.get('valu_issue_frac', 0.0) > rec['roofline']['frac']:
+            rec['roofline']['bound'] = 'valu-issue'
+            rec['roofline']['bound_note'] = ('VALU issue %.2f of peak and texture-data unit %.2f busy (PMC) against '
+                                             'HBM %.2f: the kernel is issue-bound, not bandwidth-bound'
+                                             % (tr['valu_issue_frac'], tr.get('td_busy_frac', float('nan')),
+                                                rec['roofline']['frac']))
     rec['config']['output_checksum'] = checksum
     if world == 1 and args.cpu_seconds > 0:
         rec['cpu_baseline'] = cpu_baseline(params, lattice_host, W, H, args.cpu_seconds)

@@ -10,8 +10,10 @@
 #include <string>
 #include <vector>
 
+#define H2S_PRIVATE_TEST_HOOKS
 #include "../../include/h2s.h"
 #include "h2s_device.h"
+#include "h2s_peak.h"
 
 namespace h2s {
 hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s);
@@ -27,9 +29,11 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, l
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
                              long long yuv_fp, int w, int h, uint8_t* rgb, long long rls, long long rgb_fp,
                              const uint8_t* glut, int nframes, hipStream_t s);
-constexpr int PEAK_BLOCKS = 64;  // partial (max, sum) records per frame
-constexpr int PEAK_BINS = 1024;  // percentile histogram bins over PQ [0, 1] (h2s_kernels.hip)
 hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s);
+hipError_t launch_peak_frame(const float2* partial, const unsigned* hist, const PeakModel& M, double2* fstat, int n,
+                             hipStream_t s);
+hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out,
+                              hipStream_t s);
 }  // namespace h2s
 
 using h2s::FastParams;
@@ -62,19 +66,20 @@ struct h2s_ctx {
   size_t stage_bytes = 0;
   void* d_prev = nullptr;  // preview scratch
   size_t prev_bytes = 0;
-  // dynamic peak (params.peak_detect): per-frame stats buffer + IIR state
-  void* d_stats = nullptr;       // peak statistics: per-block partials, then (percentile model) histograms
+  // dynamic peak (params.peak_detect), all on the device: statistics ->
+  // per-frame (max, avg) -> IIR + curve records -> conversion, queued on the
+  // caller's stream with no host round trip (h2s_peak.h)
+  void* d_stats = nullptr;       // per-block partials, then (percentile model) histograms
   size_t stats_cap = 0;
+  double2* d_fstat = nullptr;    // per frame: the statistic, then the smoothed (max, avg) its curve uses
+  size_t fstat_cap = 0;
   h2s::CurveConsts* d_curve = nullptr;    // one curve record per frame of a dynamic-peak launch
   size_t curve_cap = 0;
-  h2s::CurveConsts* h_curve = nullptr;    // pinned host side of the last upload (alive until it completes)
-  size_t h_curve_cap = 0;
-  void* h_stats = nullptr;                // pinned landing buffer of d_stats (stats_cap bytes)
-  hipEvent_t curve_ev = nullptr;          // recorded after the launch that reads d_curve
-  double pk_max = 0.0, pk_avg = 0.0, pk_peak = 0.0;
-  long long pk_frames = 0;
+  h2s::PeakState* d_pk = nullptr;         // [0] the smoothing state; [1] a preview's saved copy of it
+  hipEvent_t peak_ev = nullptr;           // after the last launch that used the buffers above
+  bool peak_pending = false;
   std::string err;
-  bool fail_after_launch = false;  // H2S_OPT_FAIL_AFTER_LAUNCH (test hook, one call)
+  bool fail_after_launch = false;  // H2S_OPT_TEST_FAIL_AFTER_LAUNCH (private test hook, one call)
   bool timing = false;
   hipEvent_t ev0[kEvRing] = {}, ev1[kEvRing] = {};
   long long ev_count = 0;  // launches recorded since reset
@@ -122,16 +127,9 @@ struct DeviceGuard {
 
 // ---- parameter resolution (mirrors vf_tonemap init/filter_frame, zimg,
 // vf_eq create_lut; the CPU statement is oracle/h2s_oracle.c resolve()) ----
-float hable_h(float in) {
-  const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
-  return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
-}
+float hable_h(float in) { return h2s::hd_hable(in); }
 
-double pq_encode_d(double y) {
-  const double m1 = 0.1593017578125, m2 = 78.84375, c1 = 0.8359375, c2 = 18.8515625, c3 = 18.6875;
-  double ym = pow(fmax(y, 0.0), m1);
-  return pow((c1 + c2 * ym) / (1.0 + c3 * ym), m2);
-}
+double pq_encode_d(double y) { return h2s::hd_pq_encode(y); }
 
 int validate_params(h2s_ctx* c, const h2s_params* p) {
   if (p->transfer_in != H2S_TRC_PQ && p->transfer_in != H2S_TRC_HLG)
@@ -196,93 +194,8 @@ int validate_params(h2s_ctx* c, const h2s_params* p) {
   return 0;
 }
 
-// BT.2390 EETF constants (libplacebo tone_mapping.c bt2390) for a source
-// peak (units of 100 nits) and the SDR target [k->t_black, k->t_white] nits:
-// knee ks = (1 + offset) maxLum - offset, black-point adaptation exponent
-// bp = min(1 / minLum, 4) and gain 1 / (1 + minLum / maxLum (1 - maxLum)^bp)
-// libplacebo's reinhard / hable / mobius in NORM units (1 = target white)
-// for a source peak (units of 100 nits); oracle lp_norm_curve
-void lp_norm_consts(double peak, double tm_param, KParams* k) {
-  const float pk = (float)(peak * 100.0 / k->t_white);
-  k->n_peak = pk;
-  const float ct = isnan(tm_param) ? 0.5f : (float)tm_param;
-  k->n_rein_off = (1.0f - ct) / ct;
-  k->n_rein_scale = (pk + k->n_rein_off) / pk;
-  k->n_hable_inv = 1.0f / hable_h(pk);
-  const float j = isnan(tm_param) ? 0.3f : (float)tm_param;
-  const float a = -j * j * (pk - 1.0f) / (j * j - 2.0f * j + pk);
-  const float b = (j * j - 2.0f * j * pk + pk) / fmaxf(1e-6f, pk - 1.0f);
-  k->n_mob_j = j, k->n_mob_a = a, k->n_mob_b = b;
-  k->n_mob_scale = (b * b + 2.0f * b * j + j * j) / (b - a);
-}
-
-void bt2390_consts(double peak, KParams* k) {
-  const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
-  const double ml = (pq_encode_d(k->t_white / 10000.0) - smin) / (smax - smin);
-  const double mn = k->t_black > 0.0 ? (pq_encode_d(k->t_black / 10000.0) - smin) / (smax - smin) : 0.0;
-  const double ks = (1.0 + k->knee_off) * ml - k->knee_off;
-  const double bp = mn > 0.0 ? fmin(1.0 / mn, 4.0) : 4.0;
-  k->b_srcmin = (float)smin;
-  k->b_range = (float)(smax - smin);
-  k->b_inv_range = (float)(1.0 / (smax - smin));
-  k->b_ks = (float)ks;
-  k->b_inv_1mks = (float)(1.0 / (1.0 - ks));
-  k->b_maxlum = (float)ml;
-  k->b_minlum = (float)mn;
-  k->b_bp = (float)bp;
-  k->b_gain = (float)(ml < 1.0 ? 1.0 / (1.0 + mn / ml * pow(1.0 - ml, bp)) : 1.0);
-}
-
-// ST 2084 EOTF in double (normalised: 1.0 = 10000 nits)
-double pq_eotf_d(double e);
-
-// libplacebo's "spline" tone curve (tone_mapping.c, scaling PL_HDR_PQ;
-// PARITY UNPINNED: libplacebo is absent): a single-pivot
-// curve in the PQ domain, a quadratic toe below the knee and a cubic
-// shoulder above it with zero curvature at the source peak.  The knee
-// follows pick_knee with libplacebo's default constants (knee adaptation
-// 0.4, minimum 0.1, maximum 0.8, default 0.4; slope tuning 1.5, slope offset
-// 0.2).  avg_pq: the frame's average PQ level (peak detection), 0 = unknown.
-void spline_consts(double peak, double avg_pq, double contrast, KParams* k) {
-  const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
-  auto mix = [](double a, double b, double t) { return a + (b - a) * t; };
-  auto smooth = [](double e0, double e1, double x) {
-    double t = (x - e0) / (e1 - e0);
-    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-    return t * t * (3.0 - 2.0 * t);
-  };
-  const double smin = pq_encode_d(0.0), smax = pq_encode_d(peak * 100.0 / 10000.0);
-  const double dmin = pq_encode_d(k->t_black / 10000.0), dmax = pq_encode_d(k->t_white / 10000.0);
-  double sk = avg_pq > 0.0 ? avg_pq : mix(smin, smax, kdef);
-  sk = fmin(fmax(sk, mix(smin, smax, kmin)), mix(smin, smax, kmax));
-  const double target = (sk - smin) / (smax - smin);
-  const double adapted = mix(dmin, dmax, target);
-  const double tuning = 1.0 - smooth(kmax, kdef, target) * smooth(kmin, kdef, target);
-  double dk = mix(sk, adapted, mix(kad, 1.0, tuning));
-  dk = fmin(fmax(dk, dmin), dmax);
-  double ratio = st * (smax / dmax - 1.0);
-  ratio = fmin(fmax(ratio, so), 1.0 + so);
-  const double slope = pow(pq_eotf_d(dk) / pq_eotf_d(sk), (1.0 - contrast) * ratio);
-  const double in_min = smin - sk, in_max = smax - sk, out_min = dmin - dk, out_max = dmax - dk;
-  const double tq = 2.0 * in_max * in_max;
-  k->sp_srcmin = (float)smin, k->sp_srcmax = (float)smax;
-  k->sp_kin = (float)sk, k->sp_kout = (float)dk;
-  k->sp_pa = (float)((out_min - slope * in_min) / (in_min * in_min));
-  k->sp_pb = (float)slope;
-  k->sp_qa = (float)((slope * in_max - out_max) / (in_max * tq));
-  k->sp_qb = (float)(-3.0 * (slope * in_max - out_max) / tq);
-  k->sp_qc = (float)slope;
-  k->sp_dmin = (float)dmin, k->sp_dmax = (float)dmax;
-}
-
-double pq_eotf_d(double e) {
-  const double m1 = 2610.0 / 16384.0, m2 = 2523.0 / 4096.0 * 128.0, c1 = 3424.0 / 4096.0, c2 = 2413.0 / 4096.0 * 32.0,
-               c3 = 2392.0 / 4096.0 * 32.0;
-  if (!(e > 0.0)) return 0.0;
-  const double xp = pow(e, 1.0 / m2);
-  const double num = xp - c1 > 0.0 ? xp - c1 : 0.0;
-  return pow(num / (c2 - c3 * xp), 1.0 / m1);
-}
+// the per-frame curve constants (BT.2390, spline, libplacebo's NORM curves)
+// and their folded fast-kernel form are h2s_peak.h's host/device functions
 
 // IPT-PQ matrices (h2s_lp_tone IPT), in double: BT.2020 RGB -> XYZ from the
 // primaries and D65 white, XYZ -> LMS by the Hunt-Pointer-Estevez matrix of
@@ -412,17 +325,18 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
   {
     const double lb = pow(k->t_black / k->t_white, 1.0 / 2.4), a = pow(1.0 - lb, 2.4);
     k->enc_ainv = (float)(1.0 / a);
+    k->enc_a = (float)a;
     k->enc_b = (float)(lb / (1.0 - lb));
   }
-  bt2390_consts(peak, k);
+  h2s::bt2390_consts(peak, k->t_white, k->t_black, k->knee_off, k);
   k->sp_contrast = isnan(p->tm_param) ? 0.5f : (float)p->tm_param;
-  spline_consts(peak, 0.0, k->sp_contrast, k);
+  h2s::spline_consts(peak, 0.0, (double)k->sp_contrast, k->t_white, k->t_black, k);
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / k->t_white);
-  k->ipt_npl = p->npl / 10000.0, k->ipt_os = 10000.0 / k->t_white;
+  k->ipt_npl = p->npl / 10000.0, k->ipt_os = 10000.0 / k->t_white, k->ipt_tw = k->t_white / 10000.0;
   k->lp_norm = lp && p->tonemap >= H2S_TM_REINHARD && p->tonemap <= H2S_TM_MOBIUS ? 1 : 0;
   k->n_nw = (float)(p->npl / k->t_white);
-  lp_norm_consts(peak, p->tm_param, k);
+  h2s::lp_norm_consts(peak, p->tm_param, k->t_white, k);
   // closed-form gamut step (lut_enabled = 0), tools/generate_lut.py:36-40
   const double m[9] = {1.6604910021, -0.5876411388, -0.0728498633, -0.1245504745, 1.1328998971,
                        -0.0083494226, -0.0181507634, -0.1005788980, 1.1187296614};
@@ -677,6 +591,8 @@ extern "C" {
 
 int h2s_abi_version(void) { return H2S_ABI_VERSION; }
 
+int h2s_abi_minor(void) { return H2S_ABI_MINOR; }
+
 const char* h2s_last_error(const h2s_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 void h2s_params_default(h2s_params* p) {
@@ -751,11 +667,11 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
   if (c->d_stats) hipFree(c->d_stats);
+  if (c->d_fstat) hipFree(c->d_fstat);
   if (c->d_curve) hipFree(c->d_curve);
+  if (c->d_pk) hipFree(c->d_pk);
   if (c->d_chr) hipFree(c->d_chr);
-  if (c->h_curve) hipHostFree(c->h_curve);
-  if (c->h_stats) hipHostFree(c->h_stats);
-  if (c->curve_ev) hipEventDestroy(c->curve_ev);
+  if (c->peak_ev) hipEventDestroy(c->peak_ev);
   if (c->chr_ev) hipEventDestroy(c->chr_ev);
   for (hipEvent_t ev : c->pend) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_free) hipEventDestroy(ev);
@@ -936,40 +852,6 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   return 0;
 }
 
-// BT.2390 / spline constants in the fast kernel's folded form (per launch, or
-// per frame under dynamic peak detection)
-static void curve_fast(const KParams& k, h2s::CurveConsts* cc) {
-  cc->b_srcmin = k.b_srcmin, cc->b_range = k.b_range, cc->b_inv_range = k.b_inv_range;
-  cc->b_ks = k.b_ks, cc->b_inv_1mks = k.b_inv_1mks, cc->b_maxlum = k.b_maxlum;
-  cc->b_minlum = k.b_minlum, cc->b_bp = k.b_bp, cc->b_gain = k.b_gain;
-  cc->sp_srcmin = k.sp_srcmin, cc->sp_srcmax = k.sp_srcmax, cc->sp_kin = k.sp_kin, cc->sp_kout = k.sp_kout;
-  cc->sp_pa = k.sp_pa, cc->sp_pb = k.sp_pb, cc->sp_qa = k.sp_qa, cc->sp_qb = k.sp_qb, cc->sp_qc = k.sp_qc;
-  cc->sp_dmin = k.sp_dmin, cc->sp_dmax = k.sp_dmax;
-  {
-    const double seg = h2s::PQ_SEG, smin = k.b_srcmin, range = k.b_range, ks = k.b_ks, ml = k.b_maxlum;
-    const double R = range * seg, C = smin * seg + 1.0;
-    // (2t^3-3t^2+1) ks + (t^3-2t^2+t)(1-ks) + (-2t^3+3t^2) ml as a3 t^3 + a2 t^2 + a1 t + a0
-    const double a3 = ks + 1.0 - 2.0 * ml, a2 = -ks - 2.0 + 3.0 * ml, a1 = 1.0 - ks, a0 = ks;
-    cc->b_e1a = k.b_inv_range, cc->b_e1b = (float)(-smin * (double)k.b_inv_range);
-    cc->b_ta = k.b_inv_1mks, cc->b_tb = (float)(-ks * (double)k.b_inv_1mks);
-    cc->b_c3 = (float)(R * a3), cc->b_c2 = (float)(R * a2), cc->b_c1 = (float)(R * a1), cc->b_c0 = (float)(R * a0 + C);
-    cc->b_lr = (float)R, cc->b_lc = (float)C;
-    cc->b_thr = ks < 1.0 ? (float)ks : 2.0f;   // ks >= 1: the knee is never reached
-    cc->sp_qa_u = (float)(seg * k.sp_qa), cc->sp_qb_u = (float)(seg * k.sp_qb), cc->sp_qc_u = (float)(seg * k.sp_qc);
-    cc->sp_pa_u = (float)(seg * k.sp_pa), cc->sp_pb_u = (float)(seg * k.sp_pb);
-    cc->sp_k_u = (float)(seg * k.sp_kout + 1.0);
-    cc->sp_umin = (float)(seg * k.sp_dmin + 1.0), cc->sp_umax = (float)(seg * k.sp_dmax + 1.0);
-    // black-point adaptation in u: 1 - e2 = (R + C - u) / R; u' = gain u +
-    // R gain mn (1 - e2)^bp + (1 - gain)(C + R mn)   (e2 < 1)
-    const double mn = k.b_minlum, gain = k.b_gain;
-    cc->b_bk_a = (float)(-1.0 / R), cc->b_bk_b = (float)((R + C) / R);
-    cc->b_bk_c = (float)(R * gain * mn), cc->b_bk_d = (float)((1.0 - gain) * (C + R * mn));
-  }
-  cc->n_peak = k.n_peak, cc->n_rein_off = k.n_rein_off, cc->n_rein_scale = k.n_rein_scale;
-  cc->n_hable_inv = k.n_hable_inv, cc->n_mob_j = k.n_mob_j, cc->n_mob_a = k.n_mob_a, cc->n_mob_b = k.n_mob_b;
-  cc->n_mob_scale = k.n_mob_scale;
-}
-
 // FastParams from the resolved KParams (same constants, scales folded)
 static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   memset(F, 0, sizeof(*F));
@@ -994,6 +876,7 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
     F->a_bu[odd] = (float)(mbcb * cs / d);
   }
   F->log2_lin_scale = (float)log2((p->transfer_in == H2S_TRC_HLG ? 1000.0 : 10000.0) / p->npl);
+  F->log2_pq_scale = (float)log2(10000.0 / p->npl);
   {
     // k_tile takes a tile's steps without the exact-path ballot when every
     // pixel's E stays below the table's end: staged luma <= safe_y and
@@ -1037,7 +920,7 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->n_nw = k.n_nw;
   F->tw_1e4 = (float)(k.t_white / 10000.0);
   for (int i = 0; i < 9; i++) F->m709[i] = k.m709[i];
-  curve_fast(k, F);
+  h2s::curve_fast(k, static_cast<h2s::CurveConsts*>(F));
   const int n = c->lut_n;
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);
@@ -1281,181 +1164,152 @@ static int ensure_chr(h2s_ctx* c, const KParams& k) {
   return 0;
 }
 
-// libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md):
-// IIR low-pass with time constant 20 frames on the PQ-domain frame max and
-// average, bypassed progressively for scene changes whose average moves by
-// 10..30 % PQ (smoothstep); the result is clamped to [1, static peak].
-static double peak_update(h2s_ctx* c, double fmax, double favg, double static_peak) {
-  const KParams& k = c->k;
-  if (c->pk_frames == 0) {
-    c->pk_max = fmax, c->pk_avg = favg;
-  } else {
-    // IIR with coefficient 1 - exp(-1 / smoothing_period); a scene change
-    // (frame-average jump of scene_low .. scene_high % PQ) bypasses it
-    // progressively (smoothstep); negative thresholds turn that off
-    const double a = k.pd_smoothing > 0.0 ? 1.0 - exp(-1.0 / k.pd_smoothing) : 1.0;
-    const double d = fabs(favg - c->pk_avg) * 100.0;
-    double t = 0.0;
-    if (k.pd_scene_low >= 0.0 && k.pd_scene_high >= 0.0)
-      t = k.pd_scene_high > k.pd_scene_low ? (d - k.pd_scene_low) / (k.pd_scene_high - k.pd_scene_low)
-                                           : (d >= k.pd_scene_low ? 1.0 : 0.0);
-    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-    const double w = a + (1.0 - a) * t * t * (3.0 - 2.0 * t);
-    c->pk_max += w * (fmax - c->pk_max);
-    c->pk_avg += w * (favg - c->pk_avg);
-  }
-  c->pk_frames++;
-  double peak = pq_eotf_d(c->pk_max) * 100.0;  // units of 100 nits, as vf_tonemap's peak
-  if (peak < k.pd_min) peak = k.pd_min;          // minimum_peak x the target white
-  if (peak > static_peak) peak = static_peak;
-  c->pk_peak = peak;
-  return peak;
+// libplacebo-style detected peak (PARITY UNPINNED; model in DESIGN.md §4.6),
+// all on the device (h2s_peak.h): k_peak_stats* (per-block partials and the
+// percentile histograms) -> k_peak_frame (per-frame statistic) ->
+// k_peak_curves (the IIR in frame order from the context's device state, and
+// one curve record per frame) -> the conversion, which reads the records.
+// h2s_process queues all of it on the caller's stream and returns; the state
+// comes back to the host only on demand (h2s_peak_state).
+static h2s::PeakModel peak_model(const h2s_ctx* c, const KParams& k) {
+  h2s::PeakModel m;
+  m.t_white = k.t_white, m.t_black = k.t_black, m.knee_off = k.knee_off;
+  m.contrast = k.sp_contrast, m.tm_param = c->params.tm_param, m.static_peak = k.peak;
+  m.smoothing = k.pd_smoothing, m.scene_low = k.pd_scene_low, m.scene_high = k.pd_scene_high;
+  m.percentile = k.pd_percentile, m.min_peak = k.pd_min;
+  m.npx = (double)k.W * k.H;
+  m.nblocks = h2s::PEAK_BLOCKS;
+  m.pct = k.pd_percentile < 100.0 ? 1 : 0;
+  return m;
 }
 
-// statistics for every frame in one launch, then the frames in order, each
-// with the BT.2390 / spline constants of its smoothed peak.  The fast kernel
-// takes every frame's curve in one launch (a record per frame, selected by the
-// tile's frame index), so the chip stays full; the generic kernel and the
-// ragged tail columns go frame by frame.
-// per-frame max and mean of the PQ-encoded max(R,G,B) for the batch k binds
-// (k_peak_stats_v partials, folded on the host)
-// the pct-th percentile of a frame's PQ(max R,G,B) from its histogram
-// (bins of 1/nb over [0, 1]): the first bin whose cumulative count reaches
-// pct % of the pixels, interpolated linearly inside it, capped at the frame
-// maximum (oracle_peak_stats; PARITY UNPINNED: libplacebo's own histogram
-// and interpolation are not restated)
-static double pq_percentile(const unsigned* h, int nb, double pct, double mx) {
-  double n = 0.0;
-  for (int i = 0; i < nb; i++) n += h[i];
-  const double target = pct / 100.0 * n;
-  double cum = 0.0;
-  for (int i = 0; i < nb; i++) {
-    if (h[i] && cum + h[i] >= target) {
-      const double v = (i + (target - cum) / h[i]) / nb;
-      return v < mx ? v : mx;
-    }
-    cum += h[i];
+// device buffer of at least `need` bytes (grown, never shrunk); a grown
+// buffer is freed only after the launches that read the old one (hipFree
+// synchronises)
+static int ensure_dev(h2s_ctx* c, void** buf, size_t* cap, size_t need, const char* what) {
+  if (need <= *cap) return 0;
+  if (*buf) hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  if (hipMalloc(buf, need) != hipSuccess) {
+    *buf = nullptr;
+    return fail(c, H2S_E_OOM, std::string(what) + " allocation failed");
   }
-  return mx;
-}
-
-static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, std::vector<double>* fmax,
-                       std::vector<double>* favg) {
-  const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
-  // pd_percentile < 100: a per-frame histogram of PQ(max R,G,B) as well
-  const bool pct = k.pd_percentile < 100.0;
-  const size_t hneed = pct ? (size_t)nframes * h2s::PEAK_BINS : 0;
-  // partials and histograms in one device buffer and one pinned host buffer,
-  // so that one copy brings them back (the round trip between the statistics
-  // launch and the tile launch is on every dynamic-peak call's critical path)
-  const size_t sbytes = need * sizeof(float2) + hneed * sizeof(unsigned);
-  if (sbytes > c->stats_cap) {
-    if (c->d_stats) hipFree(c->d_stats);
-    if (c->h_stats) hipHostFree(c->h_stats);
-    c->d_stats = c->h_stats = nullptr;
-    c->stats_cap = 0;
-    if (hipMalloc(&c->d_stats, sbytes) != hipSuccess || hipHostMalloc(&c->h_stats, sbytes, hipHostMallocDefault) != hipSuccess) {
-      if (c->d_stats) hipFree(c->d_stats);
-      c->d_stats = c->h_stats = nullptr;
-      return fail(c, H2S_E_OOM, "peak statistics allocation failed");
-    }
-    c->stats_cap = sbytes;
-  }
-  float2* d_part = static_cast<float2*>(c->d_stats);
-  unsigned* d_hist = reinterpret_cast<unsigned*>(d_part + need);
-  const float2* part = static_cast<const float2*>(c->h_stats);
-  const unsigned* hist = reinterpret_cast<const unsigned*>(part + need);
-  hipError_t e = pct ? hipMemsetAsync(d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
-  if (e == hipSuccess) e = h2s::launch_peak_stats(k, d_part, pct ? d_hist : nullptr, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_stats, c->d_stats, sbytes, hipMemcpyDeviceToHost, s);
-  // (polling an event instead of this blocking wait measured no better:
-  // profiles/r04/c3_dyn/round_trip_*.txt)
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(c, e, "peak statistics");
-  const double npx = (double)k.W * k.H;
-  fmax->assign(nframes, 0.0);
-  favg->assign(nframes, 0.0);
-  for (int f = 0; f < nframes; f++) {
-    double mx = 0.0, sum = 0.0;
-    for (int b = 0; b < h2s::PEAK_BLOCKS; b++) {
-      const float2 v = part[(size_t)f * h2s::PEAK_BLOCKS + b];
-      mx = v.x > mx ? v.x : mx;
-      sum += v.y;
-    }
-    (*fmax)[f] = pct ? pq_percentile(hist + (size_t)f * h2s::PEAK_BINS, h2s::PEAK_BINS, k.pd_percentile, mx) : mx;
-    (*favg)[f] = sum / npx;
-  }
+  *cap = need;
   return 0;
 }
 
+static int ensure_peak_state(h2s_ctx* c) {
+  if (c->d_pk) return 0;
+  if (hipMalloc((void**)&c->d_pk, 2 * sizeof(h2s::PeakState)) != hipSuccess) {
+    c->d_pk = nullptr;
+    return fail(c, H2S_E_OOM, "peak state allocation failed");
+  }
+  hipStream_t aux;
+  if (int rc = aux_stream(c, &aux)) return rc;
+  hipError_t e = hipMemsetAsync(c->d_pk, 0, 2 * sizeof(h2s::PeakState), aux);
+  if (e == hipSuccess) e = hipStreamSynchronize(aux);
+  return e == hipSuccess ? 0 : hip_fail(c, e, "peak state reset");
+}
+
+// the statistics, the curves and the state are one context's scratch: a call
+// on another stream waits (on the device) for the previous call's use of
+// them, so consecutive calls see the state in call order
+static int peak_order(h2s_ctx* c, hipStream_t s) {
+  if (!c->peak_ev) {
+    hipError_t e = hipEventCreateWithFlags(&c->peak_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      c->peak_ev = nullptr;
+      return hip_fail(c, e, "peak event");
+    }
+  }
+  if (!c->peak_pending) return 0;
+  hipError_t e = hipStreamWaitEvent(s, c->peak_ev, 0);
+  return e == hipSuccess ? 0 : hip_fail(c, e, "peak ordering");
+}
+
+static int peak_done(h2s_ctx* c, hipStream_t s) {
+  hipError_t e = hipEventRecord(c->peak_ev, s);
+  if (e != hipSuccess) return hip_fail(c, e, "peak event");
+  c->peak_pending = true;
+  return 0;
+}
+
+// per-frame statistic (PQ peak measurement, average PQ) of the batch k binds
+// into c->d_fstat, queued on s
+static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s) {
+  const h2s::PeakModel m = peak_model(c, k);
+  const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
+  const size_t hneed = m.pct ? (size_t)nframes * h2s::PEAK_BINS : 0;
+  if (int rc = ensure_dev(c, &c->d_stats, &c->stats_cap, need * sizeof(float2) + hneed * sizeof(unsigned),
+                          "peak statistics"))
+    return rc;
+  if (int rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)nframes * sizeof(double2), "peak statistics"))
+    return rc;
+  float2* d_part = static_cast<float2*>(c->d_stats);
+  unsigned* d_hist = reinterpret_cast<unsigned*>(d_part + need);
+  hipError_t e = m.pct ? hipMemsetAsync(d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
+  if (e == hipSuccess) e = h2s::launch_peak_stats(k, d_part, m.pct ? d_hist : nullptr, s);
+  if (e == hipSuccess) e = h2s::launch_peak_frame(d_part, m.pct ? d_hist : nullptr, m, c->d_fstat, nframes, s);
+  return e == hipSuccess ? 0 : hip_fail(c, e, "peak statistics");
+}
+
+// statistics, then the frames in order, each with the BT.2390 / spline
+// constants of its smoothed peak.  The fast kernel takes every frame's curve
+// in one launch (a record per frame, selected by the tile's frame index), so
+// the chip stays full; the generic kernel and the ragged tail columns go frame
+// by frame, each launch reading its frame's record.
 static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
-  std::vector<double> fmx, fav;
-  int rc = frame_stats(c, k, nframes, s, &fmx, &fav);
-  if (rc) return rc;
-  hipError_t e = hipSuccess;
-  std::vector<KParams> kfs(nframes, k);
+  int rc;
+  if ((rc = ensure_peak_state(c)) || (rc = peak_order(c, s))) return rc;
+  if ((rc = frame_stats(c, k, nframes, s))) return rc;
+  if ((rc = ensure_dev(c, (void**)&c->d_curve, &c->curve_cap, (size_t)nframes * sizeof(h2s::CurveConsts), "curve records")))
+    return rc;
+  hipError_t e = h2s::launch_peak_curves(c->d_fstat, nframes, peak_model(c, k), c->d_pk, c->d_curve, s);
+  if (e != hipSuccess) return hip_fail(c, e, "peak curves");
   if (fast) {
-    if (c->curve_ev && (e = hipEventSynchronize(c->curve_ev)) != hipSuccess) return hip_fail(c, e, "curve upload");
-    if ((size_t)nframes > c->h_curve_cap) {
-      if (c->h_curve) hipHostFree(c->h_curve);
-      c->h_curve = nullptr;
-      c->h_curve_cap = 0;
-      if (hipHostMalloc((void**)&c->h_curve, (size_t)nframes * sizeof(h2s::CurveConsts), hipHostMallocDefault) !=
-          hipSuccess) {
-        c->h_curve = nullptr;
-        return fail(c, H2S_E_OOM, "curve records host buffer allocation failed");
-      }
-      c->h_curve_cap = nframes;
-    }
-  }
-  for (int f = 0; f < nframes; f++) {
-    KParams& kf = kfs[f];
-    const double peak = peak_update(c, fmx[f], fav[f], k.peak);
-    bt2390_consts(peak, &kf);
-    spline_consts(peak, c->pk_avg, k.sp_contrast, &kf);
-    lp_norm_consts(peak, c->params.tm_param, &kf);
-    if (fast) curve_fast(kf, &c->h_curve[f]);
-    for (int p = 0; p < 3; p++) {
-      kf.in[p] += f * kf.in_fp[p];
-      kf.out[p] += f * kf.out_fp[p];
-    }
-    kf.nframes = 1;
-    kf.total = (long long)kf.ch * kf.ngx;
-  }
-  if (fast) {
-    if ((size_t)nframes > c->curve_cap) {
-      if (c->d_curve) hipFree(c->d_curve);
-      c->d_curve = nullptr;
-      c->curve_cap = 0;
-      if (hipMalloc((void**)&c->d_curve, (size_t)nframes * sizeof(h2s::CurveConsts)) != hipSuccess) {
-        c->d_curve = nullptr;
-        return fail(c, H2S_E_OOM, "curve records allocation failed");
-      }
-      c->curve_cap = nframes;
-    }
-    if (!c->curve_ev && (e = hipEventCreateWithFlags(&c->curve_ev, hipEventDisableTiming)) != hipSuccess) {
-      c->curve_ev = nullptr;
-      return hip_fail(c, e, "curve event");
-    }
-    e = hipMemcpyAsync(c->d_curve, c->h_curve, (size_t)nframes * sizeof(h2s::CurveConsts),
-                       hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
-    if (e == hipSuccess) e = hipEventRecord(c->curve_ev, s);
+    e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
-    if ((k.W & (h2s::TBW - 1)) == 0) return 0;
   }
-  for (int f = 0; f < nframes; f++) {
-    e = fast ? launch_tail(kfs[f], 1, vec, out8, s, h2s::TBW) : launch_chain(c, kfs[f], false, vec, out8, 1, s);
-    if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+  if (!fast || (k.W & (h2s::TBW - 1)) != 0) {
+    for (int f = 0; f < nframes; f++) {
+      KParams kf = k;
+      for (int p = 0; p < 3; p++) {
+        kf.in[p] += f * kf.in_fp[p];
+        kf.out[p] += f * kf.out_fp[p];
+      }
+      kf.nframes = 1;
+      kf.total = (long long)kf.ch * kf.ngx;
+      kf.cv = c->d_curve + f;
+      e = fast ? launch_tail(kf, 1, vec, out8, s, h2s::TBW) : launch_chain(c, kf, false, vec, out8, 1, s);
+      if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+    }
+  }
+  return peak_done(c, s);
+}
+
+// the host-side peak calls act on the state as the context's queued work
+// leaves it: they wait for that work first (its launch events and the last
+// peak launch), then run on the context stream and wait for it
+static int peak_sync(h2s_ctx* c, hipStream_t* aux) {
+  int rc;
+  if ((rc = drain_launches(c)) || (rc = ensure_peak_state(c)) || (rc = aux_stream(c, aux))) return rc;
+  if (c->peak_pending) {
+    hipError_t e = hipEventSynchronize(c->peak_ev);
+    if (e != hipSuccess) return hip_fail(c, e, "peak launches");
+    c->peak_pending = false;
   }
   return 0;
 }
 
 int h2s_peak_reset(h2s_ctx* c) {
   if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
-  c->pk_max = c->pk_avg = c->pk_peak = 0.0;
-  c->pk_frames = 0;
-  return 0;
+  DeviceGuard g(c->device);
+  hipStream_t aux;
+  if (int rc = peak_sync(c, &aux)) return rc;
+  hipError_t e = hipMemsetAsync(c->d_pk, 0, sizeof(h2s::PeakState), aux);
+  if (e == hipSuccess) e = hipStreamSynchronize(aux);
+  return e == hipSuccess ? 0 : hip_fail(c, e, "peak state reset");
 }
 
 int h2s_peak_feed(h2s_ctx* c, const double* fmax, const double* favg, int n) {
@@ -1464,16 +1318,35 @@ int h2s_peak_feed(h2s_ctx* c, const double* fmax, const double* favg, int n) {
   KParams k;
   int rc = prepare(c, &k, false);  // the statistics need no LUT
   if (rc) return rc;
-  for (int i = 0; i < n; i++) peak_update(c, fmax[i], favg[i], k.peak);
-  return 0;
+  if (n == 0) return 0;
+  DeviceGuard g(c->device);
+  hipStream_t aux;
+  if ((rc = peak_sync(c, &aux))) return rc;
+  if ((rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)n * sizeof(double2), "peak statistics"))) return rc;
+  std::vector<double2> st(n);
+  for (int i = 0; i < n; i++) st[i] = make_double2(fmax[i], favg[i]);
+  // the same device IIR as h2s_process (bit-identical state either way)
+  hipError_t e = hipMemcpyAsync(c->d_fstat, st.data(), n * sizeof(double2), hipMemcpyHostToDevice, aux);
+  if (e == hipSuccess) e = h2s::launch_peak_curves(c->d_fstat, n, peak_model(c, k), c->d_pk, nullptr, aux);
+  if (e == hipSuccess) e = hipStreamSynchronize(aux);
+  return e == hipSuccess ? 0 : hip_fail(c, e, "peak feed");
 }
 
-int h2s_peak_state(const h2s_ctx* c, double* max_pq, double* avg_pq, double* peak, int64_t* frames) {
-  if (!c) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
-  if (max_pq) *max_pq = c->pk_max;
-  if (avg_pq) *avg_pq = c->pk_avg;
-  if (peak) *peak = c->pk_peak;
-  if (frames) *frames = c->pk_frames;
+int h2s_peak_state(const h2s_ctx* cc, double* max_pq, double* avg_pq, double* peak, int64_t* frames) {
+  if (!cc) return fail(nullptr, H2S_E_INVALID_ARG, "ctx is NULL");
+  // logically const: waits for the context's queued work, copies the state back
+  h2s_ctx* c = const_cast<h2s_ctx*>(cc);
+  DeviceGuard g(c->device);
+  hipStream_t aux;
+  if (int rc = peak_sync(c, &aux)) return rc;
+  h2s::PeakState st;
+  hipError_t e = hipMemcpyAsync(&st, c->d_pk, sizeof(st), hipMemcpyDeviceToHost, aux);
+  if (e == hipSuccess) e = hipStreamSynchronize(aux);
+  if (e != hipSuccess) return hip_fail(c, e, "peak state read-back");
+  if (max_pq) *max_pq = st.max;
+  if (avg_pq) *avg_pq = st.avg;
+  if (peak) *peak = st.peak;
+  if (frames) *frames = st.frames;
   return 0;
 }
 
@@ -1487,11 +1360,15 @@ int h2s_peak_stats(h2s_ctx* c, const h2s_frames* in, int nframes, double* fmax, 
   if (in->location != H2S_LOC_DEVICE) return fail(c, H2S_E_INVALID_ARG, "h2s_peak_stats takes device frames");
   if (nframes == 0) return 0;
   DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)hip_stream;
   h2s_frames out = *in;                       // geometry only: the statistics read the input planes
   fill_geometry(&k, in, &out, nframes);
-  std::vector<double> fmx, fav;
-  if ((rc = frame_stats(c, k, nframes, (hipStream_t)hip_stream, &fmx, &fav))) return rc;
-  for (int f = 0; f < nframes; f++) fmax[f] = fmx[f], favg[f] = fav[f];
+  if ((rc = peak_order(c, s)) || (rc = frame_stats(c, k, nframes, s))) return rc;
+  std::vector<double2> st(nframes);
+  hipError_t e = hipMemcpyAsync(st.data(), c->d_fstat, nframes * sizeof(double2), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(c, e, "peak statistics read-back");
+  for (int f = 0; f < nframes; f++) fmax[f] = st[f].x, favg[f] = st[f].y;
   return 0;
 }
 
@@ -1668,7 +1545,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   }
   if (e == hipSuccess && c->fail_after_launch) {
     c->fail_after_launch = false;
-    return queued_exit(c, s, fail(c, H2S_E_HIP, "injected failure after the launch (H2S_OPT_FAIL_AFTER_LAUNCH)"));
+    return queued_exit(c, s, fail(c, H2S_E_HIP, "injected failure after the launch (H2S_OPT_TEST_FAIL_AFTER_LAUNCH)"));
   }
   if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "kernel launch"));
   if (c->timing) {
@@ -1758,7 +1635,7 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
     case H2S_OPT_HOST_SERIAL:
       c->serial_host = value != 0;
       return 0;
-    case H2S_OPT_FAIL_AFTER_LAUNCH:
+    case H2S_OPT_TEST_FAIL_AFTER_LAUNCH:
       c->fail_after_launch = value != 0;
       return 0;
     default:
@@ -1912,17 +1789,25 @@ int h2s_preview_rgb24_batch(h2s_ctx* c, const h2s_frames* in, int nframes, uint8
     // ffmpeg run (extract_frames_with_gpu_conversion_batch loops
     // extract_frame_with_gpu_conversion, src/utils.py:803-824), so peak
     // detection starts afresh on every frame: one launch per frame, state
-    // reset in between
+    // reset in between.  The context's own state (a conversion sequence the
+    // caller may be in the middle of) is saved first and restored afterwards,
+    // all stream-ordered on s
+    if ((rc = ensure_peak_state(c)) || (rc = peak_order(c, s))) return rc;
+    const size_t pb = sizeof(h2s::PeakState);
+    hipError_t e = hipMemcpyAsync(c->d_pk + 1, c->d_pk, pb, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return hip_fail(c, e, "peak state save");
     for (int f = 0; f < nframes; f++) {
       h2s_frames fi = *in, fo = y8;
       for (int k = 0; k < 3; k++) {
         fi.data[k] = (uint8_t*)in->data[k] + (long long)f * in->frame_pitch[k];
         fo.data[k] = (uint8_t*)y8.data[k] + (long long)f * y8.frame_pitch[k];
       }
-      h2s_peak_reset(c);
+      if ((e = hipMemsetAsync(c->d_pk, 0, pb, s)) != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "peak state reset"));
       if ((rc = h2s_process(c, &fi, &fo, 1, hip_stream))) return rc;
     }
-    h2s_peak_reset(c);
+    if ((e = hipMemcpyAsync(c->d_pk, c->d_pk + 1, pb, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+      return queued_exit(c, s, hip_fail(c, e, "peak state restore"));
+    if ((rc = peak_done(c, s))) return queued_exit(c, s, rc);
   } else if ((rc = h2s_process(c, in, &y8, nframes, hip_stream))) {  // one launch for the batch
     return rc;
   }

@@ -12,6 +12,8 @@
 
 namespace h2s {
 
+struct CurveConsts;
+
 struct KParams {
   // geometry (luma W x H, chroma cw x ch, ngx groups of QPT chroma columns)
   int W, H, cw, ch, ngx;
@@ -48,6 +50,7 @@ struct KParams {
   // pipeline (h2s_pipeline, resolved to CPU_CHAIN or LIBPLACEBO)
   int pipe, rgba8;
   float enc_ainv, enc_b;  // libplacebo BT.1886 encode: (x * ainv)^(1/2.4) - b
+  float enc_a;            // (the generic kernel divides by a, as the oracle)
   int lp_ipt;             // libplacebo branch: the curve on IPT-PQ intensity (h2s_lp_tone IPT)
   // libplacebo branch options (include/h2s.h ABI v3): rgba8 code =
   // floor(clamp01(v) lp_qs + lp_qo + (lp_dith ? bayer16(x, y) : 0.5));
@@ -60,7 +63,7 @@ struct KParams {
   // percentile, minimum peak (units of 100 nits)
   double pd_smoothing, pd_scene_low, pd_scene_high, pd_percentile, pd_min;
   double ipt_r2l[9], ipt_l2r[9];  // BT.2020 RGB -> LMS (HPE), inverse (row-major)
-  double ipt_npl, ipt_os;         // npl / 10000, 10000 / target white (double)
+  double ipt_npl, ipt_os, ipt_tw; // npl / 10000, 10000 / target white, target white / 10000 (double)
   // libplacebo reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = target white)
   int lp_norm;                    // the libplacebo branch with one of them
   float n_peak, n_nw;             // source peak / white; npl / white (npl units -> NORM)
@@ -83,6 +86,9 @@ struct KParams {
   float k709[3], kcb[3], kcr[3];
   int gx0;  // first column group this launch covers (tail launches)
   float2* chr444;         // BICUBIC: per-pixel (Cb, Cr) of one frame (two-pass path)
+  // dynamic peak detection (one frame per launch): the frame's curve record,
+  // written on the device by k_peak_curves; null: the constants above
+  const CurveConsts* cv;
 };
 
 constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
@@ -116,6 +122,17 @@ struct CurveConsts {
   float n_peak, n_rein_off, n_rein_scale, n_hable_inv, n_mob_j, n_mob_a, n_mob_b, n_mob_scale;
 };
 
+// a frame's curve record over the generic kernel's constants (dynamic peak)
+__device__ __forceinline__ void apply_curve(KParams& P, const CurveConsts& C) {
+  P.b_srcmin = C.b_srcmin, P.b_range = C.b_range, P.b_inv_range = C.b_inv_range, P.b_ks = C.b_ks;
+  P.b_inv_1mks = C.b_inv_1mks, P.b_maxlum = C.b_maxlum, P.b_minlum = C.b_minlum, P.b_bp = C.b_bp, P.b_gain = C.b_gain;
+  P.sp_srcmin = C.sp_srcmin, P.sp_srcmax = C.sp_srcmax, P.sp_kin = C.sp_kin, P.sp_kout = C.sp_kout;
+  P.sp_pa = C.sp_pa, P.sp_pb = C.sp_pb, P.sp_qa = C.sp_qa, P.sp_qb = C.sp_qb, P.sp_qc = C.sp_qc;
+  P.sp_dmin = C.sp_dmin, P.sp_dmax = C.sp_dmax;
+  P.n_peak = C.n_peak, P.n_rein_off = C.n_rein_off, P.n_rein_scale = C.n_rein_scale, P.n_hable_inv = C.n_hable_inv;
+  P.n_mob_j = C.n_mob_j, P.n_mob_a = C.n_mob_a, P.n_mob_b = C.n_mob_b, P.n_mob_scale = C.n_mob_scale;
+}
+
 // Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
 // with every scale folded into constants.
 struct FastParams : CurveConsts {
@@ -132,6 +149,7 @@ struct FastParams : CurveConsts {
   float ys, k_r, k_g, k_b;
   float a_rv[2], a_gv[2], a_gu[2], a_bu[2];
   float log2_lin_scale;
+  float log2_pq_scale;             // log2(10000 / npl): the PQ EOTF table's scale (the IPT decode reads it for HLG input too)
   float y_off_c, c_mid;            // k_tile staging: Y' = Y*ys + y_off_c, chroma centred on c_mid
   // S2
   float lr, lg, lb, desat;
@@ -215,11 +233,16 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 // x^p for x >= 0 (x == 0 -> 0 for p > 0)
 __device__ __forceinline__ float fpow(float x, float p) { return fexp2(p * flog2(x)); }
-// the generic chain's pow: ocml powf (faithfully rounded, as libm's powf in
-// the oracle).  The PQ exponents amplify a v_log/v_exp ulp ~100-fold
-// (m2 = 78.84; the xp - c1 cancellation), enough to flip the libplacebo
-// branch's 8-bit rgba rounding; the tile kernel keeps its own fast forms
-__device__ __forceinline__ float apow(float x, float p) { return powf(x, p); }
+// the generic chain's pow and exp: correctly rounded (the double result
+// rounded once to float), which is what the oracle's libm powf / expf give
+// in practice (scripts/c3_float_floor.py: glibc powf == the correctly
+// rounded value on every one of 6.2 M encode inputs).  The PQ exponents
+// amplify a pow ulp ~100-fold (m2 = 78.84; the xp - c1 cancellation), enough
+// to flip the libplacebo branch's 8-bit rgba rounding: the generic kernel is
+// the branch's exact path (h2s_kernels.hip is built without FMA contraction,
+// in the oracle's operation order); the tile kernel keeps its own fast forms
+__device__ __forceinline__ float apow(float x, float p) { return (float)pow((double)x, (double)p); }
+__device__ __forceinline__ float aexp(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
 
 // ST 2084 constants (exact binary values, as zimg defines them)
@@ -251,7 +274,7 @@ __device__ __forceinline__ float pq_encode(float y) {
 __device__ __forceinline__ float hlg_inv_oetf(float x) {
   x = fmaxf(x, 0.0f);
   if (x <= 0.5f) return (x * x) * (1.0f / 3.0f);
-  return (expf((x - HLG_C) / HLG_A) + HLG_B) * (1.0f / 12.0f);
+  return (aexp((x - HLG_C) / HLG_A) + HLG_B) * (1.0f / 12.0f);
 }
 
 // vf_tonemap hable()
@@ -262,35 +285,43 @@ __device__ __forceinline__ float hable(float in) {
 
 // libplacebo spline on a PQ-domain signal: quadratic toe below the knee,
 // cubic shoulder above it (constants: spline_consts in h2s_api.hip)
+// (the oracle's spline_pq_f expression: unfused where the translation unit
+// does not contract, as h2s_kernels.hip)
 template <class K>
 __device__ __forceinline__ float spline_pq(const K& P, float e) {
   const float x = fminf(fmaxf(e, P.sp_srcmin), P.sp_srcmax) - P.sp_kin;
-  const float y = x > 0.0f ? fmaf(fmaf(P.sp_qa, x, P.sp_qb), x, P.sp_qc) * x : fmaf(P.sp_pa, x, P.sp_pb) * x;
+  const float y = x > 0.0f ? ((P.sp_qa * x + P.sp_qb) * x + P.sp_qc) * x : (P.sp_pa * x + P.sp_pb) * x;
   return fminf(fmaxf(y + P.sp_kout, P.sp_dmin), P.sp_dmax);
 }
 
 // libplacebo bt2390 black-point adaptation on the normalised curve output
-// (x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum, for x < 1)
+// (x += minLum (1 - x)^bp, x = gain (x - minLum) + minLum, for x < 1): the
+// tile kernel's form (HLG input), bp = 4 as two squarings
 __device__ __forceinline__ float bt2390_black(float mn, float bp, float gain, float x) {
   if (!(mn > 0.0f) || !(x < 1.0f)) return x;
   const float om = 1.0f - x;
-  const float pw = bp == 4.0f ? (om * om) * (om * om) : apow(om, bp);
+  const float pw = bp == 4.0f ? (om * om) * (om * om) : powf(om, bp);
   x += mn * pw;
   return gain * (x - mn) + mn;
 }
 
-// libplacebo bt2390 on a PQ-domain signal (oracle bt2390_pq)
+// libplacebo bt2390 on a PQ-domain signal, in the oracle's operation order
+// (oracle bt2390_pq: divisions by the range and by 1 - ks, powf for any bp)
 __device__ __forceinline__ float bt2390_pq(const KParams& P, float e1) {
-  float e1n = (e1 - P.b_srcmin) * P.b_inv_range;
+  float e1n = (e1 - P.b_srcmin) / P.b_range;
   e1n = fmaxf(fminf(e1n, 1.0f), 0.0f);  // clip to the source range (NaN -> 1)
+  const float ks = P.b_ks, ml = P.b_maxlum;
   float e2 = e1n;
-  if (P.b_ks < 1.0f && e1n > P.b_ks) {
-    float t = (e1n - P.b_ks) * P.b_inv_1mks;
+  if (ks < 1.0f && e1n > ks) {
+    float t = (e1n - ks) / (1.0f - ks);
     float t2 = t * t, t3 = t2 * t;
-    e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * P.b_ks + (t3 - 2.0f * t2 + t) * (1.0f - P.b_ks) +
-         (-2.0f * t3 + 3.0f * t2) * P.b_maxlum;
+    e2 = (2.0f * t3 - 3.0f * t2 + 1.0f) * ks + (t3 - 2.0f * t2 + t) * (1.0f - ks) + (-2.0f * t3 + 3.0f * t2) * ml;
   }
-  e2 = bt2390_black(P.b_minlum, P.b_bp, P.b_gain, e2);
+  if (P.b_minlum > 0.0f && e2 < 1.0f) {
+    const float mn = P.b_minlum;
+    e2 += mn * apow(1.0f - e2, P.b_bp);
+    e2 = P.b_gain * (e2 - mn) + mn;
+  }
   return e2 * P.b_range + P.b_srcmin;
 }
 
@@ -311,7 +342,7 @@ __device__ __forceinline__ double pq_eotf_dd(double e) {
 __device__ __forceinline__ float lp_norm_curve(const KParams& P, float x) {
   x = fminf(fmaxf(x, 0.0f), P.n_peak);
   if (P.tonemap == 4) return P.n_rein_scale * x / (x + P.n_rein_off);
-  if (P.tonemap == 5) return hable(x) * P.n_hable_inv;
+  if (P.tonemap == 5) return hable(x) / hable(P.n_peak);   // (oracle: hable(x) / hable(pk))
   return x <= P.n_mob_j ? x : P.n_mob_scale * (x + P.n_mob_a) / (x + P.n_mob_b);
 }
 
@@ -325,7 +356,7 @@ __device__ __forceinline__ void tone_ipt(const KParams& P, float& r, float& g, f
   double I2;
   if (P.tonemap == 8) I2 = spline_pq(P, (float)I);
   else if (P.tonemap == 7) I2 = bt2390_pq(P, (float)I);
-  else I2 = pq_encode_dd((double)lp_norm_curve(P, (float)(pq_eotf_dd(I) * P.ipt_os)) / P.ipt_os);
+  else I2 = pq_encode_dd((double)lp_norm_curve(P, (float)(pq_eotf_dd(I) * P.ipt_os)) * P.ipt_tw);
   const double dI = I2 - I;
   double l[3];
 #pragma unroll
@@ -453,7 +484,7 @@ __device__ __forceinline__ void lut3d_tetra(const KParams& P, float& r, float& g
 // libplacebo branch: BT.1886 encode against the target black (oracle lp_encode)
 __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
   x = x > 0.0f ? x : 0.0f;
-  return apow(x * P.enc_ainv, 1.0f / 2.4f) - P.enc_b;
+  return apow(x / P.enc_a, 1.0f / 2.4f) - P.enc_b;
 }
 
 // libplacebo branch: rgba8 download (round to nearest), then vf_lut3d's 8-bit
@@ -461,7 +492,7 @@ __device__ __forceinline__ float lp_encode(const KParams& P, float x) {
 // 8 bits; returns the 8-bit values / 255
 // qoff: lp_qoff (the range=tv offset and the rounding / dither offset)
 __device__ __forceinline__ float rgba8_q(const KParams& P, float v, float qoff) {
-  return floorf(fmaf(clamp01(v), P.lp_qs, qoff));
+  return floorf(clamp01(v) * P.lp_qs + qoff);   // (two roundings, as the oracle's rgba8_q)
 }
 
 // 16 x 16 Bayer matrix (M_2n = 4 M_n + M_1 per 2 x 2 block, M_1 = [0 2; 3 1])

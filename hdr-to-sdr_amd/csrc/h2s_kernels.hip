@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "h2s_device.h"
+#include "h2s_peak.h"
 
 namespace h2s {
 
@@ -31,8 +32,13 @@ __device__ __forceinline__ int ld16(const uint8_t* row, int x) {
 // C444: BICUBIC chroma (two-pass path): store every pixel's (Cb, Cr) into
 // P.chr444 (frame 0 of the launch, W x H) instead of the 2x2 mean; the
 // chroma planes are then written by k_chroma_bicubic
-template <int QPT, bool VEC, bool OUT8, bool C444 = false>
-__global__ __launch_bounds__(256) void k_process(const KParams P) {
+template <int QPT, bool VEC, bool OUT8, bool C444 = false, bool DYN = false>
+__global__ __launch_bounds__(256) void k_process(const KParams P0) {
+  // DYN (dynamic peak detection, one frame per launch): the frame's curve
+  // constants come from the record k_peak_curves wrote on the device (P0.cv),
+  // not from the launch parameters
+  KParams P = P0;
+  if (DYN) apply_curve(P, *P0.cv);
   const long long lb = xcd_remap(blockIdx.x, gridDim.x);
   const long long item = lb * 256 + threadIdx.x;
   if (item >= P.total) return;
@@ -285,7 +291,10 @@ hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s) 
   const long long nb = (P.total + 255) / 256;
   if (nb == 0) return hipSuccess;
   dim3 grid((unsigned)nb), block(256);
-  if (vec) {
+  if (P.cv) {   // dynamic peak: the frame's curve record on the device
+    if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, false, true>), grid, block, 0, s, P);
+    else hipLaunchKernelGGL((k_process<QPT, false, false, false, true>), grid, block, 0, s, P);
+  } else if (vec) {
     if (out8) hipLaunchKernelGGL((k_process<QPT, true, true>), grid, block, 0, s, P);
     else hipLaunchKernelGGL((k_process<QPT, true, false>), grid, block, 0, s, P);
   } else {
@@ -314,8 +323,14 @@ hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s) {
   constexpr int QPT = 4;
   const long long nb = (P.total + 255) / 256;
   if (nb == 0) return hipSuccess;
-  if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
-  else hipLaunchKernelGGL((k_process<QPT, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  if (P.cv) {   // dynamic peak: the frame's curve record on the device
+    if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((k_process<QPT, false, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  } else if (out8) {
+    hipLaunchKernelGGL((k_process<QPT, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  } else {
+    hipLaunchKernelGGL((k_process<QPT, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+  }
   return hipGetLastError();
 }
 
@@ -353,8 +368,7 @@ __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned
 
 // percentile model (pd_percentile < 100; PARITY UNPINNED):
 // a PEAK_BINS-bin histogram of the per-pixel PQ(max R,G,B) per frame; the
-// host interpolates the percentile inside its bin (oracle_peak_stats)
-constexpr int PEAK_BINS = 1024;
+// percentile is interpolated inside its bin by k_peak_frame (oracle_peak_stats)
 // a thread's run of equal bins, added to the LDS histogram once per run: on
 // smooth content neighbouring pixels share a bin, and one LDS atomic per pixel
 // had all 64 lanes of a wave serialise on one address; the
@@ -482,10 +496,9 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
   peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
 }
 
-constexpr int PEAK_BLOCKS_K = 64;
 // hist: nframes x PEAK_BINS zeroed counters (the percentile model), or null
 hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s) {
-  const dim3 grid(PEAK_BLOCKS_K, P.nframes);
+  const dim3 grid(PEAK_BLOCKS, P.nframes);
   auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
   const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
                    al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
@@ -506,6 +519,105 @@ hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, 
     H2S_PEAK_LAUNCH(false)
   }
 #undef H2S_PEAK_LAUNCH
+  return hipGetLastError();
+}
+
+// ---- dynamic peak: per-frame statistic and curve records on the device ----
+// k_peak_frame: one block per frame folds the PEAK_BLOCKS partial (max, sum)
+// records in order (as the oracle's accumulation) and, for pd_percentile <
+// 100, takes the percentile from the frame's histogram: the first bin whose
+// cumulative count reaches pct % of the pixels, interpolated linearly inside
+// it, capped at the frame maximum (oracle_peak_stats).  Counts are integers,
+// so the block scan's u64 sums equal a serial double accumulation exactly.
+// fstat[f] = (PQ peak measurement, average PQ)
+__global__ __launch_bounds__(256) void k_peak_frame(const float2* partial, const unsigned* hist, const PeakModel M,
+                                                    double2* fstat) {
+  const int f = blockIdx.x, t = threadIdx.x;
+  __shared__ double s_mx, s_sum;
+  __shared__ unsigned long long s_scan[256];
+  __shared__ int s_bin;
+  if (t == 0) {
+    double mx = 0.0, sum = 0.0;
+    for (int b = 0; b < M.nblocks; b++) {
+      const float2 v = partial[(size_t)f * M.nblocks + b];
+      mx = v.x > mx ? v.x : mx;
+      sum += v.y;
+    }
+    s_mx = mx, s_sum = sum;
+    s_bin = PEAK_BINS;
+  }
+  double res = 0.0;
+  if (M.pct) {
+    static_assert(PEAK_BINS == 4 * 256, "four bins per thread");
+    const unsigned* h = hist + (size_t)f * PEAK_BINS;
+    const uint4 c = reinterpret_cast<const uint4*>(h)[t];
+    const unsigned cnt[4] = {c.x, c.y, c.z, c.w};
+    s_scan[t] = (unsigned long long)c.x + c.y + c.z + c.w;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {   // inclusive Hillis-Steele scan
+      const unsigned long long add = t >= o ? s_scan[t - o] : 0ull;
+      __syncthreads();
+      s_scan[t] += add;
+      __syncthreads();
+    }
+    const double n = (double)s_scan[255];
+    const double target = M.percentile / 100.0 * n;
+    double cum = (double)(s_scan[t] - ((unsigned long long)c.x + c.y + c.z + c.w));
+    int mine = PEAK_BINS;
+    double cum_at = 0.0;
+    for (int k = 0; k < 4; k++) {
+      if (mine == PEAK_BINS && cnt[k] && cum + cnt[k] >= target) mine = 4 * t + k, cum_at = cum;
+      cum += cnt[k];
+    }
+    if (mine < PEAK_BINS) atomicMin(&s_bin, mine);
+    __syncthreads();
+    if (mine < PEAK_BINS && mine == s_bin) {   // the owner of the first bin
+      const double v = (mine + (target - cum_at) / cnt[mine & 3]) / PEAK_BINS;
+      res = v < s_mx ? v : s_mx;
+      fstat[f] = make_double2(res, s_sum / M.npx);
+    } else if (t == 0 && s_bin == PEAK_BINS) {
+      fstat[f] = make_double2(s_mx, s_sum / M.npx);
+    }
+  } else {
+    __syncthreads();
+    if (t == 0) fstat[f] = make_double2(s_mx, s_sum / M.npx);
+  }
+}
+
+// k_peak_curves: the IIR over the launch's frames in order (thread 0, from
+// the state the previous calls left in *st), then each frame's peak and curve
+// record in parallel.  out = null: the state only (h2s_peak_feed).  One block
+void __global__ __launch_bounds__(64) k_peak_curves(double2* fstat, int n, const PeakModel M, PeakState* st,
+                                                    CurveConsts* out) {
+  const int t = threadIdx.x;
+  if (t == 0) {
+    PeakState s = *st;
+    for (int f = 0; f < n; f++) {
+      const double2 v = fstat[f];
+      peak_iir_step(&s, M, v.x, v.y);
+      fstat[f] = make_double2(s.max, s.avg);   // the smoothed values frame f's curve uses
+    }
+    if (n > 0) s.peak = peak_of(M, s.max);
+    *st = s;
+  }
+  __syncthreads();
+  if (!out) return;
+  for (int f = t; f < n; f += blockDim.x) {
+    const double2 v = fstat[f];
+    curve_for_peak(M, peak_of(M, v.x), v.y, &out[f]);
+  }
+}
+
+hipError_t launch_peak_frame(const float2* partial, const unsigned* hist, const PeakModel& M, double2* fstat, int n,
+                             hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_peak_frame, dim3(n), dim3(256), 0, s, partial, hist, M, fstat);
+  return hipGetLastError();
+}
+
+hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_peak_curves, dim3(1), dim3(64), 0, s, fstat, n, M, st, out);
   return hipGetLastError();
 }
 

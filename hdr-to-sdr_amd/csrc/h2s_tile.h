@@ -37,9 +37,12 @@
 //                offset table, one-key uniformity test (9 + 6 half-rate ops -> 6)
 //  H2S_EXPCLAMP  lut3d's [0, N-1] clamp as v_exp_f32's output clamp
 //  H2S_EQMAGIC   eq index by a 2^23 add and a 16-bit shift (full-rate ops)
-//  H2S_DARKEXACT exact EOTF for channels in the PQ table's first segment
-//                (E' < 1/128, below ~0.0015 nits), ballot-gated per step in
-//                both bodies
+// The PQ table's first segment (E' < 1/128, below ~0.0015 nits), where the
+// EOTF ~ (E - E0)^6.28 and no cubic holds 1e-3 relative, is staged as NaN:
+// a channel there comes out of pq_z as NaN, which the pixel's luma sum (or an
+// explicit probe) carries to one wave-wide test; the rare waves that meet it
+// evaluate those channels exactly (dark_fix).  No per-channel range test in
+// the common path.
 #ifndef H2S_TAGSEL
 #define H2S_TAGSEL 1
 #endif
@@ -48,9 +51,6 @@
 #endif
 #ifndef H2S_EQMAGIC
 #define H2S_EQMAGIC 1
-#endif
-#ifndef H2S_DARKEXACT
-#define H2S_DARKEXACT 0
 #endif
 
 namespace h2s {
@@ -81,13 +81,16 @@ __device__ __forceinline__ long long fxcd_remap(long long b, long long nb) {
   return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
 
-// exact zimg st_2084_eotf x 10000/npl (used above the table's range)
-__device__ __forceinline__ float pq_exact(const FastParams& F, float e) {
+// exact zimg st_2084_eotf x 2^log2_scale (S1: 10000/npl for PQ input; used
+// above the table's range and in its first segment)
+__device__ __forceinline__ float pq_exact_s(float e, float log2_scale) {
   const float xp = fexp2(flog2(fmaxf(e, 0.0f)) * (1.0f / PQ_M2));
   const float num = fmaxf(xp - PQ_C1, 0.0f);
   const float den = fmaxf(PQ_C2 - PQ_C3 * xp, 1.17549435e-38f);  // zimg: max(.., FLT_MIN)
-  return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + F.log2_lin_scale);
+  return fexp2(flog2(num * frcp(den)) * (1.0f / PQ_M1) + log2_scale);
 }
+__device__ __forceinline__ float pq_exact(const FastParams& F, float e) { return pq_exact_s(e, F.log2_lin_scale); }
+
 
 // Zero-segment form used by k_tile: the LDS table holds a zero segment at
 // index 0 and segment i of pq_tab at i+1, and the caller passes
@@ -106,13 +109,22 @@ __device__ __forceinline__ float pq_z(const float4* tab, float u) {
 // staged E (table-segment units, +1) at and above which pq_z is invalid
 constexpr float PQZ_LIM = PQ_EMAX * (float)PQ_SEG + 1.0f;
 
+// the EOTF-table read with its first segment (staged u in [1, 2): NaN in the
+// table) evaluated exactly instead: the dark re-run of a wave (px_chain)
+__device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log2_scale) {
+  const float v = pq_z(tab, u);
+  return u >= 1.0f && u < 2.0f ? pq_exact_s((u - 1.0f) * (1.0f / (float)PQ_SEG), log2_scale) : v;
+}
+
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
 // (build_pqi_table): the segment is the float's exponent and top two mantissa
 // bits, t the remaining 21 mantissa bits as [0, 1/4); clamped to the table's
-// octaves 2^-40 .. 2^14
+// octaves 2^-40 .. 2^14; NaN (and anything past 2^14, which the callers'
+// 1e6-npl cap keeps out) reads the NaN entry staged at [PQI_NSEG], so a NaN
+// from a dark EOTF-table read reaches the pixel's probe through the IPT form
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
   const unsigned b = __builtin_bit_cast(unsigned, y) & 0x7FFFFFFFu;
-  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG - 1);
+  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG);
   const float t = __builtin_bit_cast(float, (b & 0x1FFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
   return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
@@ -124,46 +136,29 @@ __device__ __forceinline__ float pqi(const float4* tab, float y) {
 // use its overflow-safe form
 // NOEX: the caller knows no E reaches the table's end (a tile of legal codes,
 // see k_tile): no ballot, no exact path, so a step has no branch
-template <int TRC, int ESC = 1, bool NOEX = false>
+// DARK: the table's first segment exactly (pq_z_dark) instead of the NaN
+template <int TRC, int ESC = 1, bool NOEX = false, bool DARK = false>
 __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_lds, float er, float eg, float eb,
                                           float& r, float& g, float& b) {
   if (TRC == 0) {
     // E arrives as E*PQ_SEG + 1 (pq_z)
     static_assert(TRC != 0 || ESC == PQ_SEG, "PQ staging is in table-segment units");
-    r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
+    if (DARK) {
+      r = pq_z_dark(pq_lds, er, F.log2_lin_scale), g = pq_z_dark(pq_lds, eg, F.log2_lin_scale);
+      b = pq_z_dark(pq_lds, eb, F.log2_lin_scale);
+    } else {   // a channel in the table's first segment is NaN here (px_chain's dark re-run)
+      r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
+    }
     constexpr float EI = 1.0f / (float)PQ_SEG;
-    auto dk = [](float u) { return __builtin_bit_cast(unsigned, u) - 0x3F800001u; };
-#if H2S_DARKEXACT
-    // the table's first segment (E < 1/128, staged u in (1, 2): below ~0.0015
-    // nits) is where EOTF ~ (E - E0)^6.28 and no cubic in t holds 1e-3
-    // relative; a step with such a channel evaluates those channels exactly
-    // (zimg's formula).  u in (1, 2) <=> u's bit pattern in (0x3F800000,
-    // 0x40000000): bits - 0x3F800001 is below 2^23 - 1 exactly there, and
-    // wraps high for u = 1 (E = 0, black), u < 1 and negative u.  About 1 % of
-    // the bench content's 8x8 steps and 3.6 % of the website frame's hold one
-    // (scripts/dark_step_sim.py)
-    unsigned dmin;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(dmin) : "v"(dk(er)), "v"(dk(eg)), "v"(dk(eb)));
-    const bool dark = __builtin_amdgcn_ballot_w64(dmin < 0x7FFFFFu) != 0;
-#else
-    const bool dark = false;
-#endif
     // NOEX (the fast body): the tile's codes keep every E inside the table
     // (tflag): no exact path above it, no ballot for it
-    if (NOEX) {
-      if (dark) {
-        r = dk(er) < 0x7FFFFFu ? pq_exact(F, (er - 1.0f) * EI) : r;
-        g = dk(eg) < 0x7FFFFFu ? pq_exact(F, (eg - 1.0f) * EI) : g;
-        b = dk(eb) < 0x7FFFFFu ? pq_exact(F, (eb - 1.0f) * EI) : b;
-      }
-      return false;
-    }
+    if (NOEX) return false;
     const float emax = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
     const bool high = __builtin_amdgcn_ballot_w64(emax >= PQZ_LIM) != 0;   // rare: extreme out-of-gamut codes
-    if (high || dark) {
-      r = er >= PQZ_LIM || (H2S_DARKEXACT && dk(er) < 0x7FFFFFu) ? pq_exact(F, (er - 1.0f) * EI) : r;
-      g = eg >= PQZ_LIM || (H2S_DARKEXACT && dk(eg) < 0x7FFFFFu) ? pq_exact(F, (eg - 1.0f) * EI) : g;
-      b = eb >= PQZ_LIM || (H2S_DARKEXACT && dk(eb) < 0x7FFFFFu) ? pq_exact(F, (eb - 1.0f) * EI) : b;
+    if (high) {
+      r = er >= PQZ_LIM ? pq_exact(F, (er - 1.0f) * EI) : r;
+      g = eg >= PQZ_LIM ? pq_exact(F, (eg - 1.0f) * EI) : g;
+      b = eb >= PQZ_LIM ? pq_exact(F, (eb - 1.0f) * EI) : b;
     }
     return high;
   } else {
@@ -215,10 +210,14 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // intensity of IPT-PQ instead (three LMS rows encoded through the PQ-encode
 // table, L'M'S' += I' - I decoded through the EOTF table), as the oracle's
 // tone_ipt.
-template <int TRC, int TM, int DESAT, int LP>
+// DARK: the dark re-run (px_chain): every EOTF-table read takes its first
+// segment exactly (pq_z_dark) instead of the NaN staged there.  luma: the
+// desaturation's luma (DESAT instances), the CPU chain's free NaN probe
+template <int TRC, int TM, int DESAT, int LP, bool DARK = false>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
                                      const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s,
-                                     float hable_kb) {
+                                     float hable_kb, float& luma_out) {
+  auto pz = [&](float u) { return DARK ? pq_z_dark(pq_lds, u, F.log2_pq_scale) : pq_z(pq_lds, u); };
   if (LP && TM >= 4 && TM <= 6) {
     // libplacebo's reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = the
     // target white; oracle lp_norm_curve), on the IPT intensity or as the
@@ -235,12 +234,10 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       const float q1 = pqi(pqi_lds, F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
       const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
       const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
-      const float x = pq_z(pq_lds, fmaf(I, (float)PQ_SEG, 1.0f)) * F.tw_fold;     // NORM
+      const float x = pz(fmaf(I, (float)PQ_SEG, 1.0f)) * F.tw_fold;     // NORM
       const float I2 = pqi(pqi_lds, curve(x) * F.tw_1e4);
       const float du = fmaf(I2 - I, (float)PQ_SEG, 1.0f);
-      auto lz = [&](float q) {
-        return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f));
-      };
+      auto lz = [&](float q) { return pz(__builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f)); };
       const float l0 = lz(q0), l1 = lz(q1), l2 = lz(q2);
       r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
       g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
@@ -315,9 +312,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
       const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
       const float du = curve_u(I) - I * (float)PQ_SEG;   // (I' - I) PQ_SEG + 1
-      auto lz = [&](float q) {
-        return pq_z(pq_lds, __builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f));
-      };
+      auto lz = [&](float q) { return pz(__builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f)); };
       const float l0 = lz(q0), l1 = lz(q1), l2 = lz(q2);
       r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
       g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
@@ -332,7 +327,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       e1 = pq_enc(sig * F.npl_1e4);
     }
     // EOTF(e4) * 10000/target white (TRC 0: the table is npl-scaled)
-    const float s2 = TRC == 0 ? pq_z(pq_lds, curve_u(e1)) * F.tw_fold : eotf_exact(curve_e4(e1)) * F.e4_npl;
+    const float s2 = TRC == 0 ? pz(curve_u(e1)) * F.tw_fold : eotf_exact(curve_e4(e1)) * F.e4_npl;
     const float k = safe ? s2 / sig : s2 * frcp(sig);   // IEEE division on the exact path (see below)
     r *= k, g *= k, b *= k;
     return;
@@ -344,6 +339,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
     // above 8.5e37 to zero, which Hable's num/den reaches at sig ~ 2.7e19
     if (DESAT) {
       const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
+      luma_out = luma;
       const float ob = fmaxf(luma - F.desat, 1e-6f) / fmaxf(luma, 1e-6f);
       r = r * (1.0f - ob) + luma * ob;
       g = g * (1.0f - ob) + luma * ob;
@@ -365,6 +361,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
   float sig, A = 1.0f, B = 0.0f;
   if (DESAT) {
     const float luma = DESAT == 2 ? (r + g) + b : F.lr * r + F.lg * g + F.lb * b;
+    luma_out = luma;
     const float ob = fmaxf(luma - F.desat, 1e-6f) * frcp(fmaxf(luma, 1e-6f));
     A = 1.0f - ob, B = luma * ob;
     sig = fmaxf(fmaf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), A, B), 1e-6f);
@@ -434,9 +431,28 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   auto dput = [&](float a, float b_, float c) {
     if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
   };
-  if (DBG == 1) dput(r, gg, bl);
-  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, __builtin_fmaxf(__builtin_fmaxf(er, eg), eb),
-                           K.hable_kb);
+  if (DBG == 1) {   // the stage-1 planes with the first segment exact, as the dark re-run below gives them
+    float r1, g1, b1;
+    to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r1, g1, b1);
+    dput(r1, g1, b1);
+  }
+  const float emax_s = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
+  float luma = 0.0f;
+  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
+  // The EOTF table is staged with a NaN first segment wherever it is read (S1
+  // on PQ input; the libplacebo branch's IPT decode and curve reads): a value
+  // that reached it is NaN in the tone map's output.  The CPU chain's
+  // desaturating instances see it in their luma for free, the others sum the
+  // channels; a wave that meets one re-runs S1 and S2 with that segment
+  // evaluated exactly (about 1 % of the bench content's 8x8 steps, 3.6 % of
+  // the website frame's)
+  if constexpr (TRC == 0 || LP) {
+    const float probe = (!LP && DESAT && TM <= 6) ? luma : (r + gg) + bl;
+    if (__builtin_amdgcn_ballot_w64(probe != probe)) {
+      const bool safe2 = to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r, gg, bl);
+      tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
+    }
+  }
   if (DBG == 2) dput(r, gg, bl);
   f3 o;
   if (LP && F.lut_off) {
@@ -542,6 +558,15 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     }
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     auto blend = [&](const f3 c0, const f3 c1, const f3 c2, const f3 c3) {
+      if constexpr (LP) {
+        // lut3d's 8-bit path truncates its output to 8 bits: the blend in
+        // the oracle's (vf_lut3d C) order, products and sums each rounded (no
+        // FMA), so that a blend on an integer boundary truncates alike
+        auto ch = [&](float a, float b, float c, float d) {
+          return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(w0, a), __fmul_rn(w1, b)), __fmul_rn(w2, c)), __fmul_rn(w3, d));
+        };
+        return f3{ch(c0.x, c1.x, c2.x, c3.x), ch(c0.y, c1.y, c2.y, c3.y), ch(c0.z, c1.z, c2.z, c3.z)};
+      }
       f3 r = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
       // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
       // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL);
@@ -908,7 +933,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
-  __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
+  __shared__ float4 pqi_lds[LP ? PQI_NSEG + 1 : 1];               // PQ encode (lp_tone IPT) + its NaN entry
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
@@ -941,7 +966,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
     eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
   }
-  if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = pq0;
+  // the first segment (E' < 1/128) as NaN wherever the table is the PQ EOTF
+  // (not the CPU chain's HLG table): px_chain's dark re-run evaluates it exactly
+  constexpr float QNAN = __builtin_nanf("");
+  if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = (TRC == 0 || LP) && t == 0 ? make_float4(QNAN, QNAN, QNAN, QNAN) : pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
   if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
@@ -950,6 +978,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
     for (int i = t; i < PQI_NSEG; i += 256)
       pqi_lds[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpi, 16 * i, 0, 0));
+    if (t == 0) pqi_lds[PQI_NSEG] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
   }
 
   // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block

@@ -38,13 +38,16 @@ LP_RANGE_FULL, LP_RANGE_LIMITED = 0, 1
 LP_DITHER_NONE, LP_DITHER_ORDERED = 0, 1
 LP_P010_KEEP, LP_P010_TRUNCATE = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
-OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL, OPT_FAIL_AFTER_LAUNCH = 1, 2, 3, 4
+OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL = 1, 2, 3
+# private test hook (include/h2s.h H2S_PRIVATE_TEST_HOOKS: not part of the ABI)
+OPT_TEST_FAIL_AFTER_LAUNCH = 0x7f000000 + 1
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
 ABI_VERSION = 3
+ABI_MINOR = 2   # include/h2s.h H2S_ABI_MINOR (the loaded library may be newer, not older)
 
 # every symbol include/h2s.h declares (checked by tests/test_abi_exports.py)
 EXPORTS = (
-    'h2s_abi_version', 'h2s_create', 'h2s_destroy', 'h2s_last_error',
+    'h2s_abi_version', 'h2s_abi_minor', 'h2s_create', 'h2s_destroy', 'h2s_last_error',
     'h2s_set_lut', 'h2s_params_default', 'h2s_set_params', 'h2s_process',
     'h2s_debug_float', 'h2s_cube_generate', 'h2s_cube_format', 'h2s_cube_parse',
     'h2s_kernel_ms', 'h2s_set_timing', 'h2s_preview_size', 'h2s_preview_rgb24', 'h2s_preview_rgb24_batch', 'h2s_peak_reset',
@@ -147,6 +150,7 @@ def lib() -> ctypes.CDLL:
     c_ctx = ctypes.c_void_p
     sig = {
         'h2s_abi_version': (ctypes.c_int, []),
+        'h2s_abi_minor': (ctypes.c_int, []),
         'h2s_create': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_ctx)]),
         'h2s_destroy': (None, [c_ctx]),
         'h2s_last_error': (ctypes.c_char_p, [c_ctx]),
@@ -186,6 +190,8 @@ def lib() -> ctypes.CDLL:
         fn.argtypes = args
     if L.h2s_abi_version() != ABI_VERSION:
         raise ImportError(f'libh2s ABI {L.h2s_abi_version()} != {ABI_VERSION}')
+    if L.h2s_abi_minor() < ABI_MINOR:
+        raise ImportError(f'libh2s ABI 3.{L.h2s_abi_minor()} is older than the 3.{ABI_MINOR} these bindings need')
     _lib = L
     return L
 

@@ -50,7 +50,12 @@ CFLAGS = ['-O3', '-std=c++17', '-fno-slp-vectorize', '-fPIC', '-Wno-unused-value
 # default is the faster one (C2 -0.7 % smooth, -3 % uniform noise; Mobius
 # alike; identical output: profiles/r04/ablations/sched_strategy.log), so the
 # tile TU builds with the default again (iterative-minreg stays 13 % slower)
-SOURCE_FLAGS = {}
+SOURCE_FLAGS = {
+    # the generic kernel is the chain's exact restatement (the libplacebo
+    # branch's exact path): no FMA contraction, so its float arithmetic rounds
+    # where the oracle's does
+    'h2s_kernels.hip': ['-ffp-contract=off'],
+}
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:

@@ -80,6 +80,24 @@ CPU_GPU_ONLY_ERROR = ("{tonemapper} requires GPU tonemapping; this item's settin
                       "— change the tonemapper or output bit depth.")
 
 
+# Dolby Vision profile 5 (src/ffmpeg_command.py:100-106, :117-128): the
+# reference routes it to libplacebo because libplacebo applies the RPU
+# (reshaping + the IPT-PQ-c2 colour matrix carried as side data); without it
+# "the output colors may look wrong (green/purple cast)".  The rawvideo pipe
+# the drop-in reads drops every side-data packet, so no RPU can reach libh2s:
+# the drop-in refuses such a source and the caller keeps the reference's own
+# command
+DOVI_P5_ERROR = ("Dolby Vision profile 5 needs its RPU (applied by libplacebo in the reference, "
+                 "src/ffmpeg_command.py:100-106); the rawvideo pipe drops it, so libh2s cannot convert "
+                 "this source — keep the reference command.")
+
+
+def is_dovi_profile5(properties: 'dict[str, Any] | None') -> bool:
+    """``_tonemap_plan``'s test (src/ffmpeg_command.py:104-106)."""
+    props = properties or {}
+    return bool(props.get('is_dolby_vision') and props.get('dovi_profile') == 5)
+
+
 @dataclass(frozen=True)
 class TonemapPlan:
     """The branch decision of ``_tonemap_plan`` (src/ffmpeg_command.py:87-93,
@@ -100,8 +118,7 @@ def tonemap_plan(request: Any, properties: 'dict[str, Any] | None' = None,
     use_gpu = bool(getattr(request, 'use_gpu', False))
     if int(getattr(request, 'bit_depth', 8)) >= 12:
         use_gpu = False
-    props = properties or {}
-    dovi = bool(props.get('is_dolby_vision') and props.get('dovi_profile') == 5)
+    dovi = is_dovi_profile5(properties)
     use_lp = False
     if use_gpu or dovi:
         use_lp = bool(libplacebo_available() if callable(libplacebo_available) else libplacebo_available)
@@ -193,7 +210,10 @@ class TonemapParams:
 
         * the branch: ``tonemap_plan`` (src/ffmpeg_command.py:96-144):
           ``use_gpu`` sends every operator through libplacebo, bit_depth >= 12
-          forces the CPU chain, Dolby Vision profile 5 forces libplacebo;
+          forces the CPU chain; Dolby Vision profile 5 (which the reference
+          sends to libplacebo for its RPU) raises ``ValueError`` with
+          ``DOVI_P5_ERROR``: the RPU cannot cross the rawvideo pipe, so the
+          caller keeps the reference command;
         * CPU chain (src/ffmpeg_command.py:240-247): bt.2390 / spline raise
           ``ValueError`` with the reference's message; the LUT is always on
           (``lut_enabled`` is ignored there, as ``_filter_args`` ignores it);
@@ -209,6 +229,8 @@ class TonemapParams:
         the engine itself always runs the libplacebo branch natively, so the
         default is True."""
         plan = tonemap_plan(request, properties, libplacebo_available)
+        if plan.dovi_needs_rpu:
+            raise ValueError(DOVI_P5_ERROR)
         tm = str(request.tonemapper).lower()
         bit_depth = int(getattr(request, 'bit_depth', 8))
         bits_out = 12 if bit_depth >= 12 else (10 if bit_depth == 10 else 8)
@@ -342,11 +364,12 @@ def _split_filters(chain: str) -> 'list[tuple[str, dict[str, str], list[str]]]':
 # and the values the engine models; anything else is rejected rather than
 # converted with a behaviour the string did not ask for
 _LP_OPTION_VALUES = {
-    # output size: iw/ih, or the preview's numbers (extract_frame_with_gpu_conversion
-    # passes PREVIEW_SIZE, src/utils.py:787): the resize belongs to the Previewer
-    # (h2s_preview_rgb24), so any positive integer is accepted and the chain runs
-    # at the source size
-    'w': None, 'h': None,
+    # output size: build() emits w=iw:h=ih for a conversion (src/utils.py:446):
+    # the engine runs the chain at the source size, so a numeric size would be
+    # silently ignored and is rejected.  The preview's numbers
+    # (extract_frame_with_gpu_conversion passes PREVIEW_SIZE, src/utils.py:787)
+    # are the Previewer's box: parse_preview_chain takes them out first
+    'w': {'iw'}, 'h': {'ih'},
     'colorspace': {'bt709'},
     'color_primaries': {'auto', 'bt709'},      # with / without the lut3d stage (checked after the loop)
     'color_trc': {'bt709'},
@@ -366,10 +389,7 @@ def _check_libplacebo_options(kv: 'dict[str, str]', pos: 'list[str]') -> None:
             raise ValueError(f'libplacebo option {k}={v} is not modelled '
                              f'(the reference sets {sorted(_LP_OPTION_VALUES)} and tonemapping)')
         allowed = _LP_OPTION_VALUES[k]
-        if allowed is None:   # w / h
-            if v not in ('iw', 'ih') and not (v.isdigit() and int(v) > 0):
-                raise ValueError(f'libplacebo {k}={v} is not modelled (iw / ih or a positive integer)')
-        elif v not in allowed:
+        if v not in allowed:
             raise ValueError(f'libplacebo {k}={v} is not modelled (accepted: {sorted(allowed)})')
 
 

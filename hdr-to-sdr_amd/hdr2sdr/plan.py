@@ -30,7 +30,7 @@ from typing import Any, Callable, Optional, Tuple
 
 import numpy as np
 
-from .chain import TonemapParams, parse_filter_chain
+from .chain import DOVI_P5_ERROR, TonemapParams, is_dovi_profile5, parse_filter_chain
 
 # planar 4:2:0 formats the pipe carries, by bit depth
 PIPE_PIX_FMT = {8: 'yuv420p', 10: 'yuv420p10le', 12: 'yuv420p12le'}
@@ -79,8 +79,13 @@ def plan_from_argv(argv: 'list[str]', properties: 'dict[str, Any]', hdr: 'dict[s
     hdr: ``_probe_hdr_metadata`` output (src/utils.py:329-372). Inside
     ffmpeg, vf_tonemap reads MaxCLL from frame side data. Raw pipes drop side
     data, so it is passed to libh2s explicitly here.
-    Raises ValueError for an argv without a tone-map filter graph."""
+    Raises ValueError for an argv without a tone-map filter graph, and for a
+    Dolby Vision profile 5 source (its RPU cannot cross the pipe)."""
     argv = list(argv)
+    if is_dovi_profile5(properties):
+        # src/ffmpeg_command.py:100-106: profile 5 needs the RPU libplacebo
+        # applies; the rawvideo decode pipe drops it
+        raise ValueError(DOVI_P5_ERROR)
     if '-i' not in argv or '-filter_complex' not in argv:
         raise ValueError('argv has no -i / -filter_complex: not a build() conversion command')
     exe = argv[0]

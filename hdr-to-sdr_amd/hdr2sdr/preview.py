@@ -89,8 +89,12 @@ def parse_preview_chain(chain: str, bits_in: int = 10, transfer: str = 'smpte208
     FFMPEG_FILTER / FFMPEG_FILTER_LEGACY_NO_LUT end in
     ``scale=W:H:force_original_aspect_ratio=decrease`` (src/utils.py:46-49,
     :57-60); the libplacebo preview carries the box as its ``w=`` / ``h=``
-    (src/utils.py:787).  The box goes to ``Previewer.convert``; the chain
-    itself runs at the source size and bits_out 8."""
+    (src/utils.py:787).  The box goes to ``Previewer.convert`` (an aspect
+    fit for the CPU chain's ``scale=``, exactly the box for the libplacebo
+    preview: ``Previewer.out_size``); the chain itself runs at the source size
+    and bits_out 8, so the libplacebo stage's numeric ``w=`` / ``h=`` are
+    replaced by ``iw`` / ``ih`` before ``parse_filter_chain``, which accepts
+    only those for a conversion chain."""
     box: 'tuple[int | str, int | str]' = ('iw', 'ih')
     parts = chain.rsplit(',', 1)
     if len(parts) == 2 and parts[1].startswith('scale='):
@@ -103,7 +107,11 @@ def parse_preview_chain(chain: str, bits_in: int = 10, transfer: str = 'smpte208
     else:
         m = re.search(r'libplacebo=w=(\w+):h=(\w+)', chain)
         if m:
+            for v in m.groups():
+                if v not in ('iw', 'ih') and not (v.isdigit() and int(v) > 0):
+                    raise ValueError(f'libplacebo preview size {v!r} is not modelled (iw / ih or a positive integer)')
             box = tuple(v if v in ('iw', 'ih') else int(v) for v in m.groups())   # type: ignore[assignment]
+            chain = chain[:m.start()] + 'libplacebo=w=iw:h=ih' + chain[m.end():]
     params, lut = parse_filter_chain(chain, bits_in=bits_in, bits_out=8, transfer=transfer, **overrides)
     return params, lut, box
 
@@ -182,10 +190,27 @@ class Previewer:
                 out[i] = img
         return out   # type: ignore[return-value]
 
+    def out_size(self, in_w: int, in_h: int, width: 'int | str' = PREVIEW_SIZE[0],
+                 height: 'int | str' = PREVIEW_SIZE[1]) -> Tuple[int, int]:
+        """The preview's output size for an in_w x in_h frame and the box.
+        CPU chain: FFMPEG_FILTER's ``scale=W:H:force_original_aspect_ratio=decrease``
+        (src/utils.py:46-49), an aspect fit.  libplacebo preview:
+        ``build_libplacebo_filter`` passes ``w=W:h=H`` with no aspect option
+        (src/utils.py:446, :787), and vf_libplacebo's own default
+        (force_original_aspect_ratio disabled) outputs exactly W x H, so a
+        non-16:9 source is stretched to the box as the reference does (the
+        resampling filter libplacebo uses for it is not restated: PARITY
+        UNPINNED; the swscale-style bicubic of the CPU preview is used)."""
+        bw = in_w if width == 'iw' else int(width)
+        bh = in_h if height == 'ih' else int(height)
+        if self.params.resolved_pipeline() == 'libplacebo':
+            if bw <= 0 or bh <= 0:
+                raise ValueError(f'preview box must be positive, got {bw}x{bh}')
+            return bw, bh
+        return fit_size(in_w, in_h, bw, bh)
+
     def _run(self, frames: FrameBatch, width: 'int | str', height: 'int | str', gamma: float) -> List[np.ndarray]:
-        bw = frames.width if width == 'iw' else int(width)
-        bh = frames.height if height == 'ih' else int(height)
-        ow, oh = fit_size(frames.width, frames.height, bw, bh)
+        ow, oh = self.out_size(frames.width, frames.height, width, height)
         n = frames.nframes
         out = np.empty((n, oh, ow, 3), dtype=np.uint8)
         d = frames.descriptor()

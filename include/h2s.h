@@ -42,6 +42,16 @@ extern "C" {
 #endif
 
 #define H2S_ABI_VERSION 3
+/* Minor revision within ABI 3 (h2s_abi_minor), for bindings that need to
+ * detect additions and behaviour changes that keep every v3 signature:
+ *   1: h2s_preview_rgb24_batch; the lp_p010 default TRUNCATE (the reference's
+ *      format=p010 upload; 12-bit libplacebo-branch output changes);
+ *   2: h2s_process with params.peak_detect is asynchronous on its stream (the
+ *      peak statistics, smoothing and curve constants run on the device);
+ *      h2s_peak_state / _reset / _feed wait for the context's queued work; a
+ *      preview restores the context's peak state; the failure-injection test
+ *      hook moved to the private option range (H2S_PRIVATE_TEST_HOOKS). */
+#define H2S_ABI_MINOR 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define H2S_OK 0
@@ -189,10 +199,16 @@ enum h2s_pipeline { H2S_PIPE_AUTO = 0, H2S_PIPE_CPU_CHAIN = 1, H2S_PIPE_LIBPLACE
 enum h2s_option {
   H2S_OPT_FAST_PATH = 1,       /* 1 (default): the tile kernel where it applies; 0: generic kernel only */
   H2S_OPT_TILES_PER_BLOCK = 2, /* tile kernel: 64x32 tiles one block walks (1..64, default 8)          */
-  H2S_OPT_HOST_SERIAL = 3,     /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
-  H2S_OPT_FAIL_AFTER_LAUNCH = 4 /* test hook: 1 = the next h2s_process call reports H2S_E_HIP right after
-                                   queueing its kernels (the error exits must still record the launch) */
+  H2S_OPT_HOST_SERIAL = 3      /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
 };
+/* Keys from H2S_OPT_PRIVATE_BASE up are the library's own test / debug hooks:
+ * not part of the ABI, may change or vanish in any build. */
+#define H2S_OPT_PRIVATE_BASE 0x7f000000
+#ifdef H2S_PRIVATE_TEST_HOOKS
+/* 1 = the next h2s_process call reports H2S_E_HIP right after queueing its
+ * kernels (the error exits must still record the launch) */
+#define H2S_OPT_TEST_FAIL_AFTER_LAUNCH (H2S_OPT_PRIVATE_BASE + 1)
+#endif
 
 /* Kernel path h2s_process takes for a given frame pair (h2s_query_path). */
 enum h2s_path {
@@ -277,6 +293,7 @@ typedef struct h2s_ctx h2s_ctx;
 
 /* ---- lifecycle ---------------------------------------------------------- */
 int h2s_abi_version(void);
+int h2s_abi_minor(void);   /* H2S_ABI_MINOR of the loaded library */
 
 /* Replaces spawning the ffmpeg child (src/conversion.py:209-224) and the
  * filter-graph setup it performs.  device = HIP device ordinal (the reference
@@ -302,9 +319,11 @@ int h2s_set_params(h2s_ctx *ctx, const h2s_params *p);
  * Processes nframes frames from `in` into `out`.  Both sets must have the
  * same width/height; in->bits == params.bits_in, out->bits ==
  * params.bits_out.  hip_stream is a hipStream_t (NULL = default stream).
- * Device->device runs asynchronously; any host-resident set is staged
- * through context-owned device buffers and the call returns after the copy
- * back (PCIe-inclusive path). */
+ * Device->device runs asynchronously, with params.peak_detect too (the peak
+ * statistics, the smoothing and the per-frame curves are queued on the same
+ * stream, ABI 3.2); any host-resident set is staged through context-owned
+ * device buffers and the call returns after the copy back (PCIe-inclusive
+ * path). */
 int h2s_process(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out,
                 int nframes, void *hip_stream);
 
@@ -331,7 +350,10 @@ int h2s_query_path(h2s_ctx *ctx, const h2s_frames *in, const h2s_frames *out);
  * h2s_peak_reset: forget the smoothing state (a new sequence / scene cut).
  * h2s_peak_state: the smoothed PQ-domain max / average after the last
  *   processed frame, the source peak (units of npl) it gave, and the number
- *   of frames folded in since the reset.  Any pointer may be NULL. */
+ *   of frames folded in since the reset.  Any pointer may be NULL.
+ * The state lives on the device and is updated in stream order by the
+ * h2s_process calls that use it; h2s_peak_reset / _feed / _state first wait
+ * for this context's queued work, then act synchronously. */
 int h2s_peak_reset(h2s_ctx *ctx);
 /* Frame-sharded runs (hdr2sdr/dist.py): the smoothing is a recurrence over
  * the whole sequence, so a rank that owns frames [a, b) first needs the
@@ -365,7 +387,7 @@ int h2s_peak_state(const h2s_ctx *ctx, double *max_pq, double *avg_pq, double *p
  *   :668-716, :803-824).  The CPU chain runs the batch as one tone-map
  *   launch; with params.peak_detect (the libplacebo branch) each frame starts
  *   from a fresh peak state, as each of the reference's per-frame ffmpeg runs
- *   does.  The resize and RGB kernels take the whole batch in one launch each.
+ *   does, and the context's own peak state is restored afterwards.  The resize and RGB kernels take the whole batch in one launch each.
  *   h2s_preview_rgb24 == the batch call with nframes = 1. */
 int h2s_preview_size(int in_w, int in_h, int box_w, int box_h, int *out_w, int *out_h);
 int h2s_preview_rgb24(h2s_ctx *ctx, const h2s_frames *in, uint8_t *rgb, int64_t rgb_linesize,

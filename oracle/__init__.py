@@ -125,6 +125,9 @@ def lib() -> ctypes.CDLL:
                                         ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_chroma_taps.restype = None
         L.oracle_chroma_taps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_tonemap_lin.restype = ctypes.c_int
+        L.oracle_tonemap_lin.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_void_p]
         L.oracle_preview_tail.restype = ctypes.c_int
         L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
@@ -182,6 +185,23 @@ def debug_float(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, w
     if rc:
         raise ValueError(f'oracle_debug_float failed: {rc}')
     return out
+
+
+def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray) -> np.ndarray:
+    """S2 alone (the chain's tone map, oracle tonemap_px) on linear R'G'B'
+    planes rgb[3, ...] in units of npl; float32 like the chain."""
+    shp = rgb.shape
+    a = np.ascontiguousarray(rgb, dtype=np.float32).reshape(3, -1)
+    out = np.empty_like(a)
+    lat, n = (None, 0)
+    if lattice is not None:
+        lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
+        n = round(lat.shape[0] ** (1 / 3))
+    rc = lib().oracle_tonemap_lin(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                                  a.ctypes.data, a.shape[1], out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_tonemap_lin failed: {rc}')
+    return out.reshape(shp)
 
 
 def preview_rgb24(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,

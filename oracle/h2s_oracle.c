@@ -1075,6 +1075,24 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
   return 0;
 }
 
+/* S2 alone on n given linear R'G'B' triples (planar: in_rgb[c * n + i],
+ * units of npl, as stage 1 reports them): the tone map the chain applies.
+ * Test infrastructure for the float gate's error propagation
+ * (tests/float_gate.py: the stage-2 Jacobian by central differences). */
+int oracle_tonemap_lin(const h2s_params *p, const float *lut, int lut_n, const float *in_rgb, int n, float *out_rgb) {
+  ocfg c;
+  int rc = resolve(&c, p, lut, lut_n);
+  if (rc) return rc;
+  for (int i = 0; i < n; i++) {
+    rgbf l = {in_rgb[i], in_rgb[n + i], in_rgb[2 * n + i]};
+    rgbf o = tonemap_px(&c, l);
+    out_rgb[i] = o.r;
+    out_rgb[n + i] = o.g;
+    out_rgb[2 * n + i] = o.b;
+  }
+  return 0;
+}
+
 /* resolved constants, for tests of the parameter logic; returns the
  * quantisation depth q (8 or bits_out) or a negative H2S_E_* code */
 int oracle_resolved(const h2s_params *p, double *peak, double *param, uint16_t *eq_lut, int eq_cap) {

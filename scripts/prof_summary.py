@@ -64,6 +64,20 @@ if 'FETCH_SIZE' in vals and 'WRITE_SIZE' in vals:
                          ('vmem_rd_per_px', 'SQ_INSTS_VMEM_RD')):
             if ctr in vals:
                 rec[key] = round(sum(vals[ctr]) / len(vals[ctr]) * 64 / px, 2)
+    # what binds the kernel: VALU wave-instructions
+    # issued per CU-cycle (one per cycle is the 4 SIMDs' peak for wave64 full-
+    # rate ops), the texture-data unit's busy share, per the cycles of the
+    # dispatch (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 32 CUs each)
+    if 'GRBM_GUI_ACTIVE' in vals:
+        cyc = sum(vals['GRBM_GUI_ACTIVE']) / len(vals['GRBM_GUI_ACTIVE']) / 8.0
+        rec['cycles_per_dispatch'] = round(cyc)
+        if 'SQ_INSTS_VALU' in vals:
+            rec['valu_issue_frac'] = round(sum(vals['SQ_INSTS_VALU']) / len(vals['SQ_INSTS_VALU']) / (cyc * 256), 4)
+        if 'SQ_ACTIVE_INST_VALU' in vals:
+            rec['valu_active_frac'] = round(4 * sum(vals['SQ_ACTIVE_INST_VALU']) / len(vals['SQ_ACTIVE_INST_VALU'])
+                                            / (cyc * 1024), 4)
+        if 'TD_TD_BUSY_sum' in vals:
+            rec['td_busy_frac'] = round(sum(vals['TD_TD_BUSY_sum']) / len(vals['TD_TD_BUSY_sum']) / (cyc * 256), 4)
     with open(os.path.join(d, 'traffic.json'), 'w') as f:
         json.dump(rec, f, indent=1)
     print('traffic.json:', json.dumps(rec))

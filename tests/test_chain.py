@@ -185,7 +185,14 @@ def test_libplacebo_unmodelled_options_are_rejected(chain):
 
 def test_libplacebo_numeric_size_is_the_previews_box():
     """extract_frame_with_gpu_conversion passes PREVIEW_SIZE as w/h
-    (src/utils.py:787); the chain runs at the source size and the box goes to
-    the Previewer's resize."""
-    p, lut = parse_filter_chain(_lp().replace('w=iw:h=ih', 'w=3840:h=2160'))
+    (src/utils.py:787): that is the Previewer's box (parse_preview_chain),
+    while a conversion chain with a numeric size is rejected, since the
+    engine runs conversions at the source size and would silently ignore it
+    (build() only ever emits w=iw:h=ih, src/utils.py:446)."""
+    from hdr2sdr import preview as PV
+    chain = _lp().replace('w=iw:h=ih', 'w=1920:h=1080')
+    with pytest.raises(ValueError):
+        parse_filter_chain(chain)
+    p, lut, box = PV.parse_preview_chain(chain)
     assert p.resolved_pipeline() == 'libplacebo' and p.peak_detect and lut == '<LUT>'
+    assert box == (1920, 1080)

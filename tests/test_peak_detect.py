@@ -9,9 +9,9 @@ pd_scene_low .. pd_scene_high % PQ change of the average bypasses at scene
 cuts; the result clamped to [pd_min_peak x SDR white, static peak].
 Defaults: vf_libplacebo's options (100 frames, 5.5 / 10 %, 99.995, 1.0);
 ROUND2 below is round 2's fixed model (20 frames, 10 / 30 %, maximum, 100
-nits).  The GPU path (per-frame stats kernel + host smoothing + per-frame
-curve constants) must match that restatement frame by frame, across calls
-on one context."""
+nits).  The GPU path (per-frame stats kernel, then the smoothing and the
+per-frame curve records on the device, queued with the conversion) must
+match that restatement frame by frame, across calls on one context."""
 import math
 
 import numpy as np
@@ -217,3 +217,85 @@ def test_gpu_sharded_peak_state_equals_sequential(tmname):
     assert np.array_equal(got, want[3:])
     assert r1.peak_state() == state
     r1.close()
+
+
+def _spin_cycles(seconds):
+    """torch's spin kernel argument for ~seconds on this device (its cycle
+    counter's rate, calibrated)."""
+    import time
+    import torch
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    torch.cuda._sleep(50_000_000)
+    torch.cuda.synchronize()
+    return int(50_000_000 * seconds / max(time.perf_counter() - t0, 1e-4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W,tmname', [(256, 'bt.2390'), (200, 'spline')])   # tile only; tile + generic tail
+def test_gpu_dynamic_peak_call_is_asynchronous(W, tmname):
+    """with peak_detect, h2s_process queues the
+    statistics, the smoothing and curve records (on the device) and the
+    conversion on its stream and returns, as include/h2s.h promises for
+    device frames: queued behind a ~0.3 s spin kernel on the same stream the
+    call returns long before the spin ends, and the output, the smoothing
+    state and the peak equal a call made on an idle stream."""
+    import time
+    import torch
+    from test_gpu_parity import lattice
+    H = 128
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper=tmname, peak_detect=True, maxcll=4000.0)
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10).to_torch('cuda')
+    ref = hdr2sdr.Tonemapper(0, params, lattice(65))
+    want = ref(src).to_numpy().buf
+    want_state = ref.peak_state()
+    ref.close()
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    dst = hdr2sdr.FrameBatch.empty_torch(buf.shape[0], W, H, 10, 'cuda')
+    side = torch.cuda.Stream()
+    spin = _spin_cycles(0.3)
+    try:
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(spin)
+        t0 = time.perf_counter()
+        tm.process(src, dst, side)
+        t_call = time.perf_counter() - t0
+        busy = not side.query()          # the spin (and the conversion behind it) still running
+        torch.cuda.synchronize()
+        assert t_call < 0.1 and busy, f'h2s_process(peak_detect) blocked the host for {t_call:.3f} s'
+        assert np.array_equal(dst.to_numpy().buf, want)
+        assert tm.peak_state() == want_state
+    finally:
+        tm.close()
+
+
+@pytest.mark.gpu
+def test_gpu_preview_restores_the_contexts_peak_state():
+    """a preview on a context that is in the middle of a
+    dynamic-peak conversion starts each preview frame from a fresh state (the
+    reference's per-frame ffmpeg runs) and leaves the context's own state as
+    it found it, so the conversion continues as if no preview had run."""
+    import ctypes
+    from hdr2sdr import _abi
+    from test_gpu_parity import lattice
+    W, H = 256, 128
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, bits_out=8, maxcll=4000.0)
+    seq = hdr2sdr.Tonemapper(0, params, lattice(65))
+    want = seq(hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)).buf
+    seq.close()
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    a = tm(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[:3]), W, H, 10)).buf
+    before = tm.peak_state()
+    rgb = np.empty((2, H, W, 3), np.uint8)
+    d = hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:5]), W, H, 10).descriptor()
+    L = _abi.lib()
+    rc = L.h2s_preview_rgb24_batch(tm._ctx, ctypes.byref(d), 2, rgb.ctypes.data, 3 * W, 3 * W * H, W, H, 1.0,
+                                   _abi.LOC_HOST, None)
+    assert rc == 0, L.h2s_last_error(tm._ctx)
+    assert tm.peak_state() == before
+    b = tm(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:]), W, H, 10)).buf
+    tm.close()
+    assert np.array_equal(np.concatenate([a, b]), want)

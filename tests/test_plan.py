@@ -72,6 +72,33 @@ def test_plan_rejects_non_conversion_argv():
         P.plan_from_argv(GOLD['C2']['argv'], dict(PROPS10, color_transfer='bt709'))
 
 
+RULES = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'request_rules.json')))
+
+
+@pytest.mark.parametrize('profile', [5, 8])
+def test_plan_refuses_dolby_vision_profile5(profile):
+    """the reference sends a Dolby Vision profile 5
+    source to libplacebo because libplacebo applies its RPU
+    (src/ffmpeg_command.py:100-106, :117-128); the rawvideo pipe drops the
+    RPU, so plan_from_argv refuses the argv build() made for it (the caller
+    keeps the reference command).  Profile 8 (HDR10-compatible base layer)
+    goes through.  The argv is the reference's C3 command with the filter
+    graph build() produced for the captured DoVi request."""
+    from hdr2sdr import chain as C
+    case = next(c for c in RULES['cases'] if c.get('props', {}).get('dovi_profile') == profile
+                and 'filter_complex' in c and c['pix_fmt'] == 'yuv420p10le')
+    argv = list(GOLD['C3']['argv'])
+    argv[argv.index('-filter_complex') + 1] = case['filter_complex']
+    props = dict(PROPS10, **case['props'])
+    if profile == 5:
+        with pytest.raises(ValueError) as e:
+            P.plan_from_argv(argv, props)
+        assert str(e.value) == C.DOVI_P5_ERROR
+        assert 'libplacebo=' in case['filter_complex']   # the reference's routing
+    else:
+        assert P.plan_from_argv(argv, props).params.resolved_pipeline() == 'cpu'
+
+
 def test_lut_path_unescape():
     from hdr2sdr.lut import unescape_filter_path
     assert unescape_filter_path('C\\\\:/Program Files/app/luts/rec2020_to_rec709.cube') == \

@@ -202,7 +202,10 @@ def test_gpu_preview_batch_mixed_sizes_vs_oracle(tm, use_gpu):
         op = oracle.params_from(pv.params.to_c())
     g13 = PV.adjust_gamma_lut(1.3)
     for f, (w, h), got, one, got13 in zip(frames, sizes, batch, singles, batch13):
-        ow, oh = PV.fit_size(w, h, *box)
+        ow, oh = pv.out_size(w, h, *box)
+        # the libplacebo preview outputs exactly the box (vf_libplacebo w/h,
+        # no aspect option: src/utils.py:787); the CPU chain fits the aspect
+        assert (ow, oh) == (box if pv.params.resolved_pipeline() == 'libplacebo' else PV.fit_size(w, h, *box))
         assert got.shape == (oh, ow, 3)
         assert np.array_equal(got, one)
         assert np.array_equal(got13, g13[got])          # the display gamma, fused

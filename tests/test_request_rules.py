@@ -5,7 +5,8 @@
 matrix of ``ConversionRequest`` fields and probe results
 (``tests/golden/make_golden.py rules``): use_gpu x operator x bit depth,
 lut_enabled x gamma, the CUDA-interop prefix, Dolby Vision profile 5 and an
-absent libplacebo.  ``TonemapParams.from_request`` must reproduce every case:
+absent libplacebo.  ``TonemapParams.from_request`` must reproduce every case
+(Dolby Vision profile 5 excepted: the drop-in refuses it, see below):
 
 * the same branch (``_tonemap_plan``, src/ffmpeg_command.py:96-144);
 * the same params as ``parse_filter_chain`` of the captured string
@@ -63,8 +64,23 @@ def _from_request(c, bits_in=10):
     return p, calls
 
 
+def _dovi5(case):
+    return C.is_dovi_profile5(case.get('props'))
+
+
 @pytest.mark.parametrize('case', RULES['cases'], ids=_case_id)
 def test_from_request_reproduces_build(case):
+    if _dovi5(case) and 'error' not in case:
+        # the reference routes profile 5 to libplacebo for its RPU
+        # (src/ffmpeg_command.py:100-106); the drop-in refuses it so that the
+        # caller keeps the reference command
+        plan = C.tonemap_plan(Req(**case['req']), case['props'], True)
+        assert plan.dovi_needs_rpu and plan.use_libplacebo
+        assert 'libplacebo=' in case['filter_complex']
+        with pytest.raises(ValueError) as e:
+            _from_request(case)
+        assert str(e.value) == C.DOVI_P5_ERROR
+        return
     if 'error' in case:
         with pytest.raises(ValueError) as e:
             _from_request(case)
@@ -198,6 +214,11 @@ def test_integration_stub_follows_the_same_rules(case):
     ns = _stub_ns()
     interop = case.get('encoder') == 'h264_nvenc' and case.get('interop', False)
     props = case.get('props', {})
+    if _dovi5(case) and 'error' not in case:
+        with pytest.raises(ValueError) as e:
+            ns['params_for'](Req(**case['req']), 10, props, interop)
+        assert str(e.value) == C.DOVI_P5_ERROR
+        return
     if 'error' in case:
         with pytest.raises(ValueError) as e:
             ns['params_for'](Req(**case['req']), 10, props, interop)
