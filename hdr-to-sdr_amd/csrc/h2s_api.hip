@@ -56,6 +56,7 @@ struct h2s_ctx {
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   bool fast_enabled = true;
+  bool lp_exact = false;  // H2S_OPT_LP_EXACT
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
@@ -1131,6 +1132,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
 static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   const h2s_params& p = c->params;
   if (!c->fast_enabled || !h2s::fast_supported(k.tonemap)) return false;
+  if (c->lp_exact && k.pipe == h2s::PIPE_LIBPLACEBO) return false;
   // the LUT off runs on the tile kernel for the libplacebo branch only (the
   // CPU chain's legacy closed form stays on the generic kernel)
   if (!k.lut_enabled && k.pipe != h2s::PIPE_LIBPLACEBO) return false;
@@ -1634,6 +1636,9 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
       return 0;
     case H2S_OPT_HOST_SERIAL:
       c->serial_host = value != 0;
+      return 0;
+    case H2S_OPT_LP_EXACT:
+      c->lp_exact = value != 0;
       return 0;
     case H2S_OPT_TEST_FAIL_AFTER_LAUNCH:
       c->fail_after_launch = value != 0;

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "h2s_libm.h"
+
 namespace h2s {
 
 struct CurveConsts;
@@ -233,16 +235,67 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 // x^p for x >= 0 (x == 0 -> 0 for p > 0)
 __device__ __forceinline__ float fpow(float x, float p) { return fexp2(p * flog2(x)); }
-// the generic chain's pow and exp: correctly rounded (the double result
-// rounded once to float), which is what the oracle's libm powf / expf give
-// in practice (scripts/c3_float_floor.py: glibc powf == the correctly
-// rounded value on every one of 6.2 M encode inputs).  The PQ exponents
-// amplify a pow ulp ~100-fold (m2 = 78.84; the xp - c1 cancellation), enough
-// to flip the libplacebo branch's 8-bit rgba rounding: the generic kernel is
-// the branch's exact path (h2s_kernels.hip is built without FMA contraction,
-// in the oracle's operation order); the tile kernel keeps its own fast forms
-__device__ __forceinline__ float apow(float x, float p) { return (float)pow((double)x, (double)p); }
-__device__ __forceinline__ float aexp(float x) { return (float)exp((double)x); }
+// the generic chain's pow and exp: the oracle's own, glibc 2.35 powf / expf
+// (the x86-64 FMA build: double-precision table + polynomial forms, one
+// rounding to float), over the tables scripts/gen_libm_tables.py reads out of
+// the libm the oracle links (h2s_libm.h; tests/test_libm_tables.py pins them).
+// Their last rounding is not the correctly rounded one for a few inputs in
+// 10^4, and the PQ EOTF amplifies a pow ulp ~500-fold (m2 = 78.84; the
+// xp - c1 and c2 - c3 xp cancellations): enough to flip the libplacebo
+// branch's 8-bit rgba rounding.  The generic kernel is the branch's exact
+// path (H2S_OPT_LP_EXACT; h2s_kernels.hip is built without FMA contraction, in
+// the oracle's operation order); the tile kernel keeps its own fast forms.
+__device__ __forceinline__ float libm_exp2_tail(double xd, double shift, const double* C) {
+  double kd = xd + shift;
+  const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+  kd -= shift;
+  const double r = xd - kd;
+  const unsigned long long t = libm::EXP2F_TAB[ki & 31] + (ki << 47);
+  const double s = __longlong_as_double((long long)t);
+  const double z = __builtin_fma(C[0], r, C[1]);
+  const double r2 = r * r;
+  double y = __builtin_fma(C[2], r, 1.0);
+  y = __builtin_fma(z, r2, y);
+  return (float)(y * s);
+}
+// powf for x >= 0 (the chain's uses); other bases take the double form
+__device__ __forceinline__ float libm_powf(float x, float yf) {
+  if (!(x > 0.0f) || !(x < __builtin_inff()) || yf == 0.0f || !(fabsf(yf) < __builtin_inff()))
+    return (float)pow((double)x, (double)yf);
+  unsigned ix = __float_as_uint(x);
+  if (ix < 0x00800000u) ix = __float_as_uint(x * 0x1p23f) - (23u << 23);  // subnormal
+  const unsigned tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) & 15u);
+  const unsigned top = tmp & 0xff800000u;
+  const unsigned iz = ix - top;
+  const int k = (int)top >> 23;
+  const double invc = libm::POWF_LOG2_TAB[i][0], logc = libm::POWF_LOG2_TAB[i][1];
+  const double z = (double)__uint_as_float(iz);
+  const double* A = libm::POWF_LOG2_POLY;
+  const double r = __builtin_fma(z, invc, -1.0);
+  const double y0 = logc + (double)k;
+  const double r2 = r * r;
+  double y = __builtin_fma(A[0], r, A[1]);
+  const double p = __builtin_fma(A[2], r, A[3]);
+  const double r4 = r2 * r2;
+  double q = __builtin_fma(A[4], r, y0);
+  q = __builtin_fma(p, r2, q);
+  y = __builtin_fma(y, r4, q);
+  const double ylogx = (double)yf * y;
+  if ((((unsigned long long)__double_as_longlong(ylogx) >> 47) & 0xffffu) >= (0x405f800000000000ull >> 47)) {
+    if (ylogx > 0x1.fffffffd1d571p+6) return __builtin_inff();
+    if (ylogx <= -150.0) return 0.0f;
+  }
+  return libm_exp2_tail(ylogx, libm::EXP2F_SHIFT_SCALED, libm::EXP2F_POLY);
+}
+__device__ __forceinline__ float libm_expf(float x) {
+  if (x != x) return x;
+  if (x > 0x1.62e42ep6f) return __builtin_inff();
+  if (x < -0x1.9fe368p6f) return 0.0f;
+  return libm_exp2_tail(libm::EXP2F_INVLN2_SCALED * (double)x, libm::EXP2F_SHIFT, libm::EXP2F_POLY_SCALED);
+}
+__device__ __forceinline__ float apow(float x, float p) { return libm_powf(x, p); }
+__device__ __forceinline__ float aexp(float x) { return libm_expf(x); }
 __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
 
 // ST 2084 constants (exact binary values, as zimg defines them)

@@ -38,11 +38,12 @@
 //  H2S_EXPCLAMP  lut3d's [0, N-1] clamp as v_exp_f32's output clamp
 //  H2S_EQMAGIC   eq index by a 2^23 add and a 16-bit shift (full-rate ops)
 // The PQ table's first segment (E' < 1/128, below ~0.0015 nits), where the
-// EOTF ~ (E - E0)^6.28 and no cubic holds 1e-3 relative, is staged as NaN:
-// a channel there comes out of pq_z as NaN, which the pixel's luma sum (or an
-// explicit probe) carries to one wave-wide test; the rare waves that meet it
-// evaluate those channels exactly (dark_fix).  No per-channel range test in
-// the common path.
+// EOTF ~ (E - E0)^6.28 and no cubic holds 1e-3 relative, is staged as the
+// cubic FLT_MAX t: exactly 0 at E = 0 (black, common in real content), and
+// above DARK_MARK for every E in (0, 1/128).  The pixel's luma sum (or an
+// explicit probe) carries such a channel to one wave-wide test; the rare
+// waves that meet it re-run S1 and S2 with those channels exact.  No
+// per-channel range test in the common path.
 #ifndef H2S_TAGSEL
 #define H2S_TAGSEL 1
 #endif
@@ -109,22 +110,26 @@ __device__ __forceinline__ float pq_z(const float4* tab, float u) {
 // staged E (table-segment units, +1) at and above which pq_z is invalid
 constexpr float PQZ_LIM = PQ_EMAX * (float)PQ_SEG + 1.0f;
 
-// the EOTF-table read with its first segment (staged u in [1, 2): NaN in the
-// table) evaluated exactly instead: the dark re-run of a wave (px_chain)
+// legitimate table values stay below ~1e10 (E < 1.875); the marked first
+// segment gives >= FLT_MAX 2^-23 = 4e31 for any E > 0
+constexpr float DARK_MARK = 1e30f;
+
+// the EOTF-table read with its first segment (staged u in (1, 2)) evaluated
+// exactly instead: the dark re-run of a wave (px_chain).  Only the lanes in
+// that segment take the exact form (a divergent branch inside the rare re-run)
 __device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log2_scale) {
-  const float v = pq_z(tab, u);
-  return u >= 1.0f && u < 2.0f ? pq_exact_s((u - 1.0f) * (1.0f / (float)PQ_SEG), log2_scale) : v;
+  float v = pq_z(tab, u);
+  if (u > 1.0f && u < 2.0f) v = pq_exact_s((u - 1.0f) * (1.0f / (float)PQ_SEG), log2_scale);
+  return v;
 }
 
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
 // (build_pqi_table): the segment is the float's exponent and top two mantissa
 // bits, t the remaining 21 mantissa bits as [0, 1/4); clamped to the table's
-// octaves 2^-40 .. 2^14; NaN (and anything past 2^14, which the callers'
-// 1e6-npl cap keeps out) reads the NaN entry staged at [PQI_NSEG], so a NaN
-// from a dark EOTF-table read reaches the pixel's probe through the IPT form
+// octaves 2^-40 .. 2^14
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
   const unsigned b = __builtin_bit_cast(unsigned, y) & 0x7FFFFFFFu;
-  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG);
+  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG - 1);
   const float t = __builtin_bit_cast(float, (b & 0x1FFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
   return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
@@ -146,7 +151,7 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
     if (DARK) {
       r = pq_z_dark(pq_lds, er, F.log2_lin_scale), g = pq_z_dark(pq_lds, eg, F.log2_lin_scale);
       b = pq_z_dark(pq_lds, eb, F.log2_lin_scale);
-    } else {   // a channel in the table's first segment is NaN here (px_chain's dark re-run)
+    } else {   // a channel in the table's first segment is marked here (px_chain's dark re-run)
       r = pq_z(pq_lds, er), g = pq_z(pq_lds, eg), b = pq_z(pq_lds, eb);
     }
     constexpr float EI = 1.0f / (float)PQ_SEG;
@@ -235,6 +240,7 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
       const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
       const float x = pz(fmaf(I, (float)PQ_SEG, 1.0f)) * F.tw_fold;     // NORM
+      luma_out = x;   // (marked for a dark I: the curve's clamp below would drop it; px_chain probes it)
       const float I2 = pqi(pqi_lds, curve(x) * F.tw_1e4);
       const float du = fmaf(I2 - I, (float)PQ_SEG, 1.0f);
       auto lz = [&](float q) { return pz(__builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f)); };
@@ -437,18 +443,31 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     dput(r1, g1, b1);
   }
   const float emax_s = __builtin_fmaxf(__builtin_fmaxf(er, eg), eb);
+  // S1's own marked channels are probed before the tone map wherever the
+  // tone map can drop the mark: the libplacebo branch's IPT form caps its
+  // input at 1e6 npl, and a max(R,G,B) gain without desaturation scales the
+  // marked channel back to the curve's output (k = curve(sig) / sig)
+  constexpr bool S1P = TRC == 0 && (LP || !(DESAT && TM <= 6));
+  const float s1probe = S1P ? (r + gg) + bl : 0.0f;
   float luma = 0.0f;
   tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
-  // The EOTF table is staged with a NaN first segment wherever it is read (S1
-  // on PQ input; the libplacebo branch's IPT decode and curve reads): a value
-  // that reached it is NaN in the tone map's output.  The CPU chain's
-  // desaturating instances see it in their luma for free, the others sum the
-  // channels; a wave that meets one re-runs S1 and S2 with that segment
-  // evaluated exactly (about 1 % of the bench content's 8x8 steps, 3.6 % of
-  // the website frame's)
+  // The EOTF table's first segment is marked wherever it is read (S1 on PQ
+  // input; the libplacebo branch's IPT decode and curve reads): a value that
+  // reached it is huge (> DARK_MARK) in S1's output or the tone map's.  The
+  // CPU chain's desaturating instances see it in their luma for free, the
+  // others sum the channels' magnitudes (and S1's, S1P); a wave that meets one re-runs S1 and S2
+  // with that segment evaluated exactly (about 1 % of the bench content's
+  // 8x8 steps)
   if constexpr (TRC == 0 || LP) {
-    const float probe = (!LP && DESAT && TM <= 6) ? luma : (r + gg) + bl;
-    if (__builtin_amdgcn_ballot_w64(probe != probe)) {
+    float probe;
+    if constexpr (!LP && DESAT && TM <= 6) {
+      probe = luma;
+    } else {
+      probe = (fabsf(r) + fabsf(gg)) + fabsf(bl);   // (the IPT rows mix signs: magnitudes do not cancel)
+      if constexpr (S1P) probe += s1probe;
+      if constexpr (LP && TM >= 4 && TM <= 6) probe += luma;   // the NORM curve's decoded intensity
+    }
+    if (__builtin_amdgcn_ballot_w64(!(probe <= DARK_MARK))) {   // (NaN / inf from a marked value too)
       const bool safe2 = to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r, gg, bl);
       tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
     }
@@ -933,7 +952,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
-  __shared__ float4 pqi_lds[LP ? PQI_NSEG + 1 : 1];               // PQ encode (lp_tone IPT) + its NaN entry
+  __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
@@ -966,10 +985,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
     eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
   }
-  // the first segment (E' < 1/128) as NaN wherever the table is the PQ EOTF
-  // (not the CPU chain's HLG table): px_chain's dark re-run evaluates it exactly
-  constexpr float QNAN = __builtin_nanf("");
-  if (stage_pq && t < PQ_NSEG) pq_lds[t + 1] = (TRC == 0 || LP) && t == 0 ? make_float4(QNAN, QNAN, QNAN, QNAN) : pq0;
+  // the first segment (E' < 1/128) marked (cubic FLT_MAX t: 0 at E = 0,
+  // > DARK_MARK above) wherever the table is the PQ EOTF (not the CPU chain's
+  // HLG table): px_chain's dark re-run evaluates it exactly
+  if (stage_pq && t < PQ_NSEG)
+    pq_lds[t + 1] = (TRC == 0 || LP) && t == 0 ? make_float4(0.0f, 0.0f, 3.40282347e38f, 0.0f) : pq0;
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
   if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
@@ -978,7 +998,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
     const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
     for (int i = t; i < PQI_NSEG; i += 256)
       pqi_lds[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpi, 16 * i, 0, 0));
-    if (t == 0) pqi_lds[PQI_NSEG] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
   }
 
   // ---- per-lane step geometry: wave w, step s -> 8x8 sub-block

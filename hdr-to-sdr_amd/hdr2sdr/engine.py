@@ -127,7 +127,7 @@ class Tonemapper:
         return dst
 
     def set_option(self, key: int, value: int) -> None:
-        """h2s_set_option (_abi.OPT_FAST_PATH / OPT_TILES_PER_BLOCK / OPT_HOST_SERIAL)."""
+        """h2s_set_option (_abi.OPT_FAST_PATH / OPT_TILES_PER_BLOCK / OPT_HOST_SERIAL / OPT_LP_EXACT)."""
         self._check(self._L.h2s_set_option(self._ctx, int(key), int(value)))
 
     def query_path(self, src: FrameBatch, dst: FrameBatch) -> int:

@@ -89,3 +89,69 @@ def test_c3_as_the_reference_runs_it_4k_sequence(tm):
     assert len(set(round(p, 3) for p in peaks)) >= 2, peaks        # the peak really moves
     assert state['frames'] == 5 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
     assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
+
+
+def _lp_exact_bound(params, got, want, W, H):
+    """H2S_OPT_LP_EXACT: every output sample within one step of the oracle's
+    (no k8 lattice-flip allowance, no share beyond)."""
+    import numpy as np
+    import oracle
+    from test_gpu_parity import parity_report
+    op = oracle.params_from(params.to_c())
+    q = oracle.quant_bits(op)
+    step = 1 << max(0, params.bits_out - q)
+    parity_report(params, got, want, W, H, q)
+    d = np.abs(got - want)
+    assert d.max(initial=0) <= step, f'max diff {d.max()} > one step ({step}); {(d > step).sum()} samples beyond'
+
+
+@pytest.mark.parametrize('kind', ['smooth', 'website'])
+def test_c3_lp_exact_full_size_within_one_step(kind):
+    """C3 (4K BT.2390, libplacebo branch, 65^3) with H2S_OPT_LP_EXACT on a
+    smooth synthetic frame and the reference's own website frame: max diff
+    one output step."""
+    import os
+    import numpy as np
+    import oracle
+    from hdr2sdr import _abi
+    from hdr2sdr.synth import synth_frames, frames_from_rgb8
+    from test_gpu_parity import lattice
+    W, H = 3840, 2160
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', gamma=1.0, bits_out=10)
+    if kind == 'website':
+        z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'website_hdr_full.npz'))
+        src = frames_from_rgb8(z[z.files[0]], 1, 10)
+    else:
+        src = synth_frames(kind, 1, W, H, 10, device='cpu', seed=11)
+    t = hdr2sdr.Tonemapper(0, params, lattice(65))
+    t.set_option(_abi.OPT_LP_EXACT, 1)
+    got = t(src.to_torch('cuda')).to_numpy().buf.astype(np.int64)
+    t.close()
+    want = oracle.process(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, W, H).astype(np.int64)
+    _lp_exact_bound(params, got, want, W, H)
+
+
+def test_c3_lp_exact_4k_sequence_within_one_step():
+    """The 5-frame C3 peak_detect sequence above, with H2S_OPT_LP_EXACT: max
+    diff one output step on every frame."""
+    import json
+    import os
+    import numpy as np
+    import oracle
+    from hdr2sdr import _abi
+    from test_gpu_parity import lattice
+    from test_peak_detect import sequence
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'filter_chains.json')
+    with open(golden) as fh:
+        chain = json.load(fh)['C3']['filter_complex']
+    params, _ = hdr2sdr.parse_filter_chain(chain, bits_out=10, maxcll=4000.0)
+    W, H = 3840, 2160
+    buf = sequence(W, H)[:5]
+    t = hdr2sdr.Tonemapper(0, params, lattice(65))
+    t.set_option(_abi.OPT_LP_EXACT, 1)
+    src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)
+    dst = hdr2sdr.FrameBatch.empty_numpy(5, W, H, 10)
+    t.process(src, dst)
+    t.close()
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    _lp_exact_bound(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
