@@ -29,9 +29,7 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, l
 hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up, const uint8_t* vp, long long cls,
                              long long yuv_fp, int w, int h, uint8_t* rgb, long long rls, long long rgb_fp,
                              const uint8_t* glut, int nframes, hipStream_t s);
-hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s);
-hipError_t launch_peak_frame(const float2* partial, const unsigned* hist, const PeakModel& M, double2* fstat, int n,
-                             hipStream_t s);
+hipError_t launch_peak_stats(const KParams& P, float2* partial, const PeakTail& T, hipStream_t s);
 hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out,
                               hipStream_t s);
 }  // namespace h2s
@@ -57,9 +55,11 @@ struct h2s_ctx {
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   bool fast_enabled = true;
   bool lp_exact = false;  // H2S_OPT_LP_EXACT
+  int peak_form = 0;      // H2S_OPT_TEST_PEAK_FORM (private A/B hook)
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
+  bool eq_ident = false;   // the resolved eq table maps every code to itself
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   float4* d_hlg = nullptr; // HLG inverse-OETF cubic segments (fast path, CPU chain)
   float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
@@ -71,7 +71,7 @@ struct h2s_ctx {
   // per-frame (max, avg) -> IIR + curve records -> conversion, queued on the
   // caller's stream with no host round trip (h2s_peak.h)
   void* d_stats = nullptr;       // per-block partials, then (percentile model) histograms
-  size_t stats_cap = 0;
+  int stats_nf = 0;   // frames d_stats is laid out for (frame_stats)
   double2* d_fstat = nullptr;    // per frame: the statistic, then the smoothed (max, avg) its curve uses
   size_t fstat_cap = 0;
   h2s::CurveConsts* d_curve = nullptr;    // one curve record per frame of a dynamic-peak launch
@@ -406,13 +406,14 @@ static void solve_cubic(const double t[4], const double y[4], double c[4]) {
 }
 
 void build_pqi_table(std::vector<float4>* out) {
+  constexpr int K = h2s::PQI_PER_OCT;
   out->resize(h2s::PQI_NSEG);
   double t[4];
-  for (int k = 0; k < 4; k++) t[k] = (1.0 - cos((2 * k + 1) * M_PI / 8.0)) / 2.0 * 0.25;
+  for (int k = 0; k < 4; k++) t[k] = (1.0 - cos((2 * k + 1) * M_PI / 8.0)) / 2.0 / K;
   for (int sg = 0; sg < h2s::PQI_NSEG; sg++) {
-    const double base = ldexp(1.0, h2s::PQI_OCT0 + sg / 4);
+    const double base = ldexp(1.0, h2s::PQI_OCT0 + sg / K);
     double y[4], c[4];
-    for (int k = 0; k < 4; k++) y[k] = pq_encode_d(base * (1.0 + (sg % 4) * 0.25 + t[k]));
+    for (int k = 0; k < 4; k++) y[k] = pq_encode_d(base * (1.0 + (double)(sg % K) / K + t[k]));
     solve_cubic(t, y, c);
     (*out)[sg] = make_float4((float)c[3], (float)c[2], (float)c[1], (float)c[0]);
   }
@@ -814,6 +815,8 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   }
   hipError_t e = table_copy(c, c->d_eq, eq.data(), eq.size() * sizeof(uint16_t));
   if (e != hipSuccess) return hip_fail(c, e, "eq table upload");
+  c->eq_ident = true;
+  for (int i = 0; i <= k.qmax && i < (int)eq.size(); i++) c->eq_ident = c->eq_ident && eq[i] == i;
   {
     std::vector<float4> pq;
     // (x 10000/npl for either input transfer: the libplacebo branch's IPT form
@@ -938,6 +941,7 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->lut_bytes = 12 * n * n * n;
   F->eq_lut = c->d_eq;
   F->eq_n = k.qmax + 1;
+  F->eq_ident = c->eq_ident && k.shift_out == 0 ? 1 : 0;
   F->c_bias = 128.0f * k.qscale + 0.5f;
   F->shift_out = k.shift_out;
   F->rep_rs = k.expand_rep && k.shift_out ? 8 - k.shift_out : 31;
@@ -1179,6 +1183,7 @@ static h2s::PeakModel peak_model(const h2s_ctx* c, const KParams& k) {
   m.contrast = k.sp_contrast, m.tm_param = c->params.tm_param, m.static_peak = k.peak;
   m.smoothing = k.pd_smoothing, m.scene_low = k.pd_scene_low, m.scene_high = k.pd_scene_high;
   m.percentile = k.pd_percentile, m.min_peak = k.pd_min;
+  m.iir_a = k.pd_smoothing > 0.0 ? 1.0 - exp(-1.0 / k.pd_smoothing) : 1.0;
   m.npx = (double)k.W * k.H;
   m.nblocks = h2s::PEAK_BLOCKS;
   m.pct = k.pd_percentile < 100.0 ? 1 : 0;
@@ -1238,21 +1243,43 @@ static int peak_done(h2s_ctx* c, hipStream_t s) {
 }
 
 // per-frame statistic (PQ peak measurement, average PQ) of the batch k binds
-// into c->d_fstat, queued on s
-static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s) {
+// into c->d_fstat, queued on s as two launches (k_peak_stats*, then
+// k_peak_finish: one block per frame folds its records; the last one, st set,
+// runs the IIR from *st and writes the curve records to out).  d_stats holds,
+// for stats_nf frames: partial records | histograms | the finish counter; the
+// histograms and the counter are zero between launches (cleared at
+// allocation, left zero by the kernels)
+static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, h2s::PeakState* st,
+                       h2s::CurveConsts* out) {
   const h2s::PeakModel m = peak_model(c, k);
-  const size_t need = (size_t)nframes * h2s::PEAK_BLOCKS;
-  const size_t hneed = m.pct ? (size_t)nframes * h2s::PEAK_BINS : 0;
-  if (int rc = ensure_dev(c, &c->d_stats, &c->stats_cap, need * sizeof(float2) + hneed * sizeof(unsigned),
-                          "peak statistics"))
-    return rc;
+  if (nframes > c->stats_nf) {
+    const size_t nf = (size_t)nframes;
+    const size_t part = nf * h2s::PEAK_BLOCKS * sizeof(float2), zero = (nf * h2s::PEAK_BINS + 1) * sizeof(unsigned);
+    if (c->d_stats) hipFree(c->d_stats);
+    c->d_stats = nullptr;
+    c->stats_nf = 0;
+    if (hipMalloc(&c->d_stats, part + zero) != hipSuccess) {
+      c->d_stats = nullptr;
+      return fail(c, H2S_E_OOM, "peak statistics allocation failed");
+    }
+    hipError_t e = hipMemsetAsync(static_cast<char*>(c->d_stats) + part, 0, zero, s);
+    if (e != hipSuccess) return hip_fail(c, e, "peak statistics clear");
+    c->stats_nf = nframes;
+  }
   if (int rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)nframes * sizeof(double2), "peak statistics"))
     return rc;
+  const size_t nf = (size_t)c->stats_nf;
   float2* d_part = static_cast<float2*>(c->d_stats);
-  unsigned* d_hist = reinterpret_cast<unsigned*>(d_part + need);
-  hipError_t e = m.pct ? hipMemsetAsync(d_hist, 0, hneed * sizeof(unsigned), s) : hipSuccess;
-  if (e == hipSuccess) e = h2s::launch_peak_stats(k, d_part, m.pct ? d_hist : nullptr, s);
-  if (e == hipSuccess) e = h2s::launch_peak_frame(d_part, m.pct ? d_hist : nullptr, m, c->d_fstat, nframes, s);
+  h2s::PeakTail T;
+  T.M = m;
+  T.fstat = c->d_fstat;
+  T.hist = reinterpret_cast<unsigned*>(d_part + nf * h2s::PEAK_BLOCKS);
+  T.done = T.hist + nf * h2s::PEAK_BINS;
+  T.st = st;
+  T.out = out;
+  T.nframes = nframes;
+  T.form = c->peak_form;
+  hipError_t e = h2s::launch_peak_stats(k, d_part, T, s);
   return e == hipSuccess ? 0 : hip_fail(c, e, "peak statistics");
 }
 
@@ -1264,11 +1291,10 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s)
 static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes, hipStream_t s) {
   int rc;
   if ((rc = ensure_peak_state(c)) || (rc = peak_order(c, s))) return rc;
-  if ((rc = frame_stats(c, k, nframes, s))) return rc;
   if ((rc = ensure_dev(c, (void**)&c->d_curve, &c->curve_cap, (size_t)nframes * sizeof(h2s::CurveConsts), "curve records")))
     return rc;
-  hipError_t e = h2s::launch_peak_curves(c->d_fstat, nframes, peak_model(c, k), c->d_pk, c->d_curve, s);
-  if (e != hipSuccess) return hip_fail(c, e, "peak curves");
+  if ((rc = frame_stats(c, k, nframes, s, c->d_pk, c->d_curve))) return rc;
+  hipError_t e;
   if (fast) {
     e = launch_chain(c, k, true, vec, out8, nframes, s, c->d_curve, false);
     if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
@@ -1365,7 +1391,7 @@ int h2s_peak_stats(h2s_ctx* c, const h2s_frames* in, int nframes, double* fmax, 
   hipStream_t s = (hipStream_t)hip_stream;
   h2s_frames out = *in;                       // geometry only: the statistics read the input planes
   fill_geometry(&k, in, &out, nframes);
-  if ((rc = peak_order(c, s)) || (rc = frame_stats(c, k, nframes, s))) return rc;
+  if ((rc = peak_order(c, s)) || (rc = frame_stats(c, k, nframes, s, nullptr, nullptr))) return rc;
   std::vector<double2> st(nframes);
   hipError_t e = hipMemcpyAsync(st.data(), c->d_fstat, nframes * sizeof(double2), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -1642,6 +1668,9 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
       return 0;
     case H2S_OPT_TEST_FAIL_AFTER_LAUNCH:
       c->fail_after_launch = value != 0;
+      return 0;
+    case H2S_OPT_TEST_PEAK_FORM:
+      c->peak_form = (int)value;
       return 0;
     default:
       return fail(c, H2S_E_INVALID_ARG, "unknown option");

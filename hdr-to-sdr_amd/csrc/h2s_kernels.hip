@@ -410,147 +410,39 @@ __device__ __forceinline__ void peak_reduce(float mx, float sm, float2* out) {
   if (threadIdx.x == 0) *out = make_float2(smx[0], ssm[0]);
 }
 
-// generic form: any width / alignment, 2-byte loads
-template <int TRC, bool HIST>
-__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial, unsigned* hist) {
-  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
-  if (HIST)
-    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
-  if (HIST) __syncthreads();
-  const int f = blockIdx.y, b = blockIdx.x;
-  float mx = 0.0f, sm = 0.0f;
-  HistRun run;
-  for (int y = b; y < P.H; y += gridDim.x) {
-    const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
-    const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
-    const uint16_t* vr = reinterpret_cast<const uint16_t*>(P.in[2] + f * P.in_fp[2] + (y >> 1) * P.in_ls[2]);
-    float rs = 0.0f;
-    for (int x = threadIdx.x; x < P.W; x += blockDim.x) {
-      const float m = peak_px<TRC>(P, yr[x], ur[x >> 1], vr[x >> 1]);
-      mx = fmaxf(mx, m);
-      rs += m;
-      if (HIST) run.add(lh, m);
-    }
-    sm += rs;
-  }
-  if (HIST) run.flush(lh);
-  if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
-  peak_reduce(mx, sm, &partial[f * gridDim.x + b]);
-}
-
-// streaming form (W % 8 == 0, 16-byte luma / 8-byte chroma alignment): each
-// thread takes 8-pixel chunks (one 16-byte luma load, one 8-byte load per
-// chroma plane), two chunks per iteration so two loads per plane are in flight
-template <int TRC, bool HIST>
-__global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, unsigned* hist) {
-  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
-  if (HIST)
-    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
-  if (HIST) __syncthreads();
-  const int f = blockIdx.y;
-  const int cpr = P.W >> 3;                       // chunks per row
-  const int nch = P.H * cpr, stride = gridDim.x * 256;
-  const uint8_t* y0 = P.in[0] + f * P.in_fp[0];
-  const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
-  const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
-  float mx = 0.0f, sm = 0.0f;
-  HistRun run;
-  auto chunk = [&](int i, uint4& ya, uint2& ua, uint2& va) {
-    const int y = i / cpr, cx = i - y * cpr;
-    ya = reinterpret_cast<const uint4*>(y0 + y * P.in_ls[0])[cx];
-    ua = reinterpret_cast<const uint2*>(u0 + (y >> 1) * P.in_ls[1])[cx];
-    va = reinterpret_cast<const uint2*>(v0 + (y >> 1) * P.in_ls[2])[cx];
-  };
-  auto fold = [&](const uint4 ya, const uint2 ua, const uint2 va) {
-    const unsigned yy[8] = {ya.x & 0xffff, ya.x >> 16, ya.y & 0xffff, ya.y >> 16,
-                            ya.z & 0xffff, ya.z >> 16, ya.w & 0xffff, ya.w >> 16};
-    const unsigned uu[4] = {ua.x & 0xffff, ua.x >> 16, ua.y & 0xffff, ua.y >> 16};
-    const unsigned vv[4] = {va.x & 0xffff, va.x >> 16, va.y & 0xffff, va.y >> 16};
-    float rs = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
-      mx = fmaxf(mx, m);
-      rs += m;
-      if (HIST) run.add(lh, m);
-    }
-    sm += rs;
-  };
-  int i = blockIdx.x * 256 + threadIdx.x;
-  for (; i + stride < nch; i += 2 * stride) {
-    uint4 ya0, ya1;
-    uint2 ua0, ua1, va0, va1;
-    chunk(i, ya0, ua0, va0);
-    chunk(i + stride, ya1, ua1, va1);
-    fold(ya0, ua0, va0);
-    fold(ya1, ua1, va1);
-  }
-  if (i < nch) {
-    uint4 ya;
-    uint2 ua, va;
-    chunk(i, ya, ua, va);
-    fold(ya, ua, va);
-  }
-  if (HIST) run.flush(lh);
-  if (HIST) hist_flush(lh, hist + (size_t)f * PEAK_BINS);
-  peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
-}
-
-// hist: nframes x PEAK_BINS zeroed counters (the percentile model), or null
-hipError_t launch_peak_stats(const KParams& P, float2* partial, unsigned* hist, hipStream_t s) {
-  const dim3 grid(PEAK_BLOCKS, P.nframes);
-  auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
-  const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
-                   al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
-                   al(P.in_fp[1], 8) && al((long long)(uintptr_t)P.in[2], 8) && al(P.in_ls[2], 8) &&
-                   al(P.in_fp[2], 8);
-#define H2S_PEAK_LAUNCH(HI)                                                                   \
-  if (vec && P.transfer == 1)                                                                 \
-    hipLaunchKernelGGL((k_peak_stats_v<1, HI>), grid, dim3(256), 0, s, P, partial, hist);     \
-  else if (vec)                                                                               \
-    hipLaunchKernelGGL((k_peak_stats_v<0, HI>), grid, dim3(256), 0, s, P, partial, hist);     \
-  else if (P.transfer == 1)                                                                   \
-    hipLaunchKernelGGL((k_peak_stats<1, HI>), grid, dim3(256), 0, s, P, partial, hist);       \
-  else                                                                                        \
-    hipLaunchKernelGGL((k_peak_stats<0, HI>), grid, dim3(256), 0, s, P, partial, hist);
-  if (hist) {
-    H2S_PEAK_LAUNCH(true)
-  } else {
-    H2S_PEAK_LAUNCH(false)
-  }
-#undef H2S_PEAK_LAUNCH
-  return hipGetLastError();
-}
-
 // ---- dynamic peak: per-frame statistic and curve records on the device ----
-// k_peak_frame: one block per frame folds the PEAK_BLOCKS partial (max, sum)
-// records in order (as the oracle's accumulation) and, for pd_percentile <
-// 100, takes the percentile from the frame's histogram: the first bin whose
-// cumulative count reaches pct % of the pixels, interpolated linearly inside
-// it, capped at the frame maximum (oracle_peak_stats).  Counts are integers,
-// so the block scan's u64 sums equal a serial double accumulation exactly.
-// fstat[f] = (PQ peak measurement, average PQ)
-__global__ __launch_bounds__(256) void k_peak_frame(const float2* partial, const unsigned* hist, const PeakModel M,
-                                                    double2* fstat) {
-  const int f = blockIdx.x, t = threadIdx.x;
+// One frame's (PQ peak measurement, average PQ) from its PEAK_BLOCKS partial
+// (max, sum) records, folded in order (as the oracle's accumulation), and for
+// pd_percentile < 100 the percentile from the frame's histogram: the first
+// bin whose cumulative count reaches pct % of the pixels, interpolated
+// linearly inside it, capped at the frame maximum (oracle_peak_stats).  Counts
+// are integers, so the block scan's u64 sums equal a serial double
+// accumulation exactly.  The histogram is left zeroed for the next call.
+// 256 threads.
+__device__ void peak_frame_fold(const float2* partial, unsigned* hist, const PeakModel& M, double2* fstat, int f) {
+  const int t = threadIdx.x;
   __shared__ double s_mx, s_sum;
   __shared__ unsigned long long s_scan[256];
   __shared__ int s_bin;
+  __shared__ float2 s_part[PEAK_BLOCKS];
+  static_assert(PEAK_BLOCKS <= 256, "one partial record per thread");
+  if (t < M.nblocks) s_part[t] = partial[(size_t)f * M.nblocks + t];   // all loads in flight at once
+  __syncthreads();
   if (t == 0) {
     double mx = 0.0, sum = 0.0;
     for (int b = 0; b < M.nblocks; b++) {
-      const float2 v = partial[(size_t)f * M.nblocks + b];
+      const float2 v = s_part[b];
       mx = v.x > mx ? v.x : mx;
       sum += v.y;
     }
     s_mx = mx, s_sum = sum;
     s_bin = PEAK_BINS;
   }
-  double res = 0.0;
   if (M.pct) {
     static_assert(PEAK_BINS == 4 * 256, "four bins per thread");
-    const unsigned* h = hist + (size_t)f * PEAK_BINS;
-    const uint4 c = reinterpret_cast<const uint4*>(h)[t];
+    uint4* h = reinterpret_cast<uint4*>(hist + (size_t)f * PEAK_BINS);
+    const uint4 c = h[t];
+    h[t] = make_uint4(0u, 0u, 0u, 0u);
     const unsigned cnt[4] = {c.x, c.y, c.z, c.w};
     s_scan[t] = (unsigned long long)c.x + c.y + c.z + c.w;
     __syncthreads();
@@ -573,8 +465,7 @@ __global__ __launch_bounds__(256) void k_peak_frame(const float2* partial, const
     __syncthreads();
     if (mine < PEAK_BINS && mine == s_bin) {   // the owner of the first bin
       const double v = (mine + (target - cum_at) / cnt[mine & 3]) / PEAK_BINS;
-      res = v < s_mx ? v : s_mx;
-      fstat[f] = make_double2(res, s_sum / M.npx);
+      fstat[f] = make_double2(v < s_mx ? v : s_mx, s_sum / M.npx);
     } else if (t == 0 && s_bin == PEAK_BINS) {
       fstat[f] = make_double2(s_mx, s_sum / M.npx);
     }
@@ -584,11 +475,10 @@ __global__ __launch_bounds__(256) void k_peak_frame(const float2* partial, const
   }
 }
 
-// k_peak_curves: the IIR over the launch's frames in order (thread 0, from
-// the state the previous calls left in *st), then each frame's peak and curve
-// record in parallel.  out = null: the state only (h2s_peak_feed).  One block
-void __global__ __launch_bounds__(64) k_peak_curves(double2* fstat, int n, const PeakModel M, PeakState* st,
-                                                    CurveConsts* out) {
+// The IIR over n frames in order (thread 0, from the state the previous calls
+// left in *st), then each frame's peak and curve record in parallel.
+// out = null: the state only.  Every thread of the block calls it.
+__device__ void peak_curves_body(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out) {
   const int t = threadIdx.x;
   if (t == 0) {
     PeakState s = *st;
@@ -608,11 +498,195 @@ void __global__ __launch_bounds__(64) k_peak_curves(double2* fstat, int n, const
   }
 }
 
-hipError_t launch_peak_frame(const float2* partial, const unsigned* hist, const PeakModel& M, double2* fstat, int n,
-                             hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_peak_frame, dim3(n), dim3(256), 0, s, partial, hist, M, fstat);
+// k_peak_finish: one block per frame folds that frame's records (and clears
+// its histogram for the next call); the last frame to finish (a device-scope
+// counter after a release fence: one per frame, so the fences stay few) runs
+// the IIR and the curve records for all of the launch's frames.  PeakTail
+// (h2s_peak.h) names the buffers; the counter is zero on entry and left zero.
+__global__ __launch_bounds__(256) void k_peak_finish(const float2* partial, const PeakTail T) {
+  const int f = blockIdx.x;
+  __shared__ int s_last;
+  peak_frame_fold(partial, T.hist, T.M, T.fstat, f);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();   // fstat[f] and the cleared histogram, device-wide
+    s_last = atomicAdd(T.done, 1u) == (unsigned)T.nframes - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) *T.done = 0u;
+  if (T.st) peak_curves_body(T.fstat, T.nframes, T.M, T.st, T.out);
+}
+
+// generic form: any width / alignment, 2-byte loads
+template <int TRC, bool HIST>
+__global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial, const PeakTail T) {
+  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (HIST)
+    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
+  if (HIST) __syncthreads();
+  const int f = blockIdx.y, b = blockIdx.x;
+  float mx = 0.0f, sm = 0.0f;
+  HistRun run;
+  for (int y = b; y < P.H; y += gridDim.x) {
+    const uint16_t* yr = reinterpret_cast<const uint16_t*>(P.in[0] + f * P.in_fp[0] + y * P.in_ls[0]);
+    const uint16_t* ur = reinterpret_cast<const uint16_t*>(P.in[1] + f * P.in_fp[1] + (y >> 1) * P.in_ls[1]);
+    const uint16_t* vr = reinterpret_cast<const uint16_t*>(P.in[2] + f * P.in_fp[2] + (y >> 1) * P.in_ls[2]);
+    float rs = 0.0f;
+    for (int x = threadIdx.x; x < P.W; x += blockDim.x) {
+      const float m = peak_px<TRC>(P, yr[x], ur[x >> 1], vr[x >> 1]);
+      mx = fmaxf(mx, m);
+      rs += m;
+      if (HIST) run.add(lh, m);
+    }
+    sm += rs;
+  }
+  if (HIST) run.flush(lh);
+  if (HIST) hist_flush(lh, T.hist + (size_t)f * PEAK_BINS);
+  peak_reduce(mx, sm, &partial[f * gridDim.x + b]);
+}
+
+// streaming form (W % 8 == 0, 16-byte luma / 8-byte chroma alignment): each
+// thread takes 8-pixel row chunks (one 16-byte luma load, one 8-byte load per
+// chroma plane), two chunks per iteration so two loads per plane are in flight.
+// ROW2 (A/B, H2S_OPT_TEST_PEAK_FORM 1; PQ input): a 2 x 8 luma chunk with its 4
+// chroma samples (one chroma row feeds two luma rows), the chroma terms
+// maximised once per sample (max(Y + dr, Y + dg, Y + db) == Y + max(dr, dg, db):
+// rounding is monotonic).  Fewer loads and VALU per pixel, yet measured 165 us
+// against 104 us for 16 4K frames (round 5, profiles/r05/peak_ab): the default
+// stays the row form
+template <int TRC, bool HIST, bool ROW2 = false>
+__global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, const PeakTail T) {
+  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (HIST)
+    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
+  if (HIST) __syncthreads();
+  const int f = blockIdx.y;
+  const int cpr = P.W >> 3;                       // chunks per row
+  const int rows = ROW2 ? (P.H + 1) >> 1 : P.H;   // chunk rows: luma row pairs (PQ) or rows
+  const int nch = rows * cpr, stride = gridDim.x * 256;
+  const uint8_t* y0 = P.in[0] + f * P.in_fp[0];
+  const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
+  const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
+  const unsigned m2 = P.in_mask | (P.in_mask << 16);
+  float mx = 0.0f, sm = 0.0f;
+  HistRun run;
+  struct Chunk {
+    uint4 ya, yb;
+    uint2 ua, va;
+    bool two;
+  };
+  auto load = [&](int i, Chunk& c) {
+    const int r = i / cpr, cx = i - r * cpr;
+    if (ROW2) {
+      const int y = 2 * r;
+      c.two = y + 1 < P.H;
+      c.ya = reinterpret_cast<const uint4*>(y0 + y * P.in_ls[0])[cx];
+      c.yb = c.two ? reinterpret_cast<const uint4*>(y0 + (y + 1) * P.in_ls[0])[cx] : c.ya;
+      c.ua = reinterpret_cast<const uint2*>(u0 + r * P.in_ls[1])[cx];
+      c.va = reinterpret_cast<const uint2*>(v0 + r * P.in_ls[2])[cx];
+    } else {
+      c.two = false;
+      c.ya = reinterpret_cast<const uint4*>(y0 + r * P.in_ls[0])[cx];
+      c.ua = reinterpret_cast<const uint2*>(u0 + (r >> 1) * P.in_ls[1])[cx];
+      c.va = reinterpret_cast<const uint2*>(v0 + (r >> 1) * P.in_ls[2])[cx];
+    }
+  };
+  auto fold = [&](const Chunk& c) {
+    const unsigned uu[4] = {c.ua.x & 0xffff, c.ua.x >> 16, c.ua.y & 0xffff, c.ua.y >> 16};
+    const unsigned vv[4] = {c.va.x & 0xffff, c.va.x >> 16, c.va.y & 0xffff, c.va.y >> 16};
+    float rs = 0.0f;
+    if (ROW2) {
+      float d[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const float cb = (float)(uu[k] & P.in_mask) * P.c_scale + P.c_off;
+        const float cr = (float)(vv[k] & P.in_mask) * P.c_scale + P.c_off;
+        d[k] = fmaxf(fmaxf(P.m_rcr * cr, P.m_gcb * cb + P.m_gcr * cr), P.m_bcb * cb);
+      }
+      auto row = [&](const uint4 ya) {
+        const unsigned w[4] = {ya.x & m2, ya.y & m2, ya.z & m2, ya.w & m2};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const unsigned code = (k & 1) ? w[k >> 1] >> 16 : w[k >> 1] & 0xffff;
+          const float m = clamp01((float)code * P.y_scale + P.y_off + d[k >> 1]);
+          mx = fmaxf(mx, m);
+          rs += m;
+          if (HIST) run.add(lh, m);
+        }
+      };
+      row(c.ya);
+      if (c.two) row(c.yb);
+    } else {
+      const unsigned yy[8] = {c.ya.x & 0xffff, c.ya.x >> 16, c.ya.y & 0xffff, c.ya.y >> 16,
+                              c.ya.z & 0xffff, c.ya.z >> 16, c.ya.w & 0xffff, c.ya.w >> 16};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
+        mx = fmaxf(mx, m);
+        rs += m;
+        if (HIST) run.add(lh, m);
+      }
+    }
+    sm += rs;
+  };
+  int i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < nch; i += 2 * stride) {
+    Chunk c0, c1;
+    load(i, c0);
+    load(i + stride, c1);
+    fold(c0);
+    fold(c1);
+  }
+  if (i < nch) {
+    Chunk c;
+    load(i, c);
+    fold(c);
+  }
+  if (HIST) run.flush(lh);
+  if (HIST) hist_flush(lh, T.hist + (size_t)f * PEAK_BINS);
+  peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
+}
+
+// the statistics of P's frames, then (k_peak_finish) their (measurement,
+// average) in T.fstat and, T.st set, the smoothed state and curve records:
+// two launches
+hipError_t launch_peak_stats(const KParams& P, float2* partial, const PeakTail& T, hipStream_t s) {
+  if (P.nframes <= 0) return hipSuccess;
+  const dim3 grid(PEAK_BLOCKS, P.nframes);
+  auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
+  const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
+                   al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
+                   al(P.in_fp[1], 8) && al((long long)(uintptr_t)P.in[2], 8) && al(P.in_ls[2], 8) &&
+                   al(P.in_fp[2], 8);
+#define H2S_PEAK_LAUNCH(HI)                                                                   \
+  if (vec && P.transfer == 1)                                                                 \
+    hipLaunchKernelGGL((k_peak_stats_v<1, HI>), grid, dim3(256), 0, s, P, partial, T);        \
+  else if (vec && T.form == 1)                                                                \
+    hipLaunchKernelGGL((k_peak_stats_v<0, HI, true>), grid, dim3(256), 0, s, P, partial, T);  \
+  else if (vec)                                                                               \
+    hipLaunchKernelGGL((k_peak_stats_v<0, HI>), grid, dim3(256), 0, s, P, partial, T);        \
+  else if (P.transfer == 1)                                                                   \
+    hipLaunchKernelGGL((k_peak_stats<1, HI>), grid, dim3(256), 0, s, P, partial, T);          \
+  else                                                                                        \
+    hipLaunchKernelGGL((k_peak_stats<0, HI>), grid, dim3(256), 0, s, P, partial, T);
+  if (T.M.pct) {
+    H2S_PEAK_LAUNCH(true)
+  } else {
+    H2S_PEAK_LAUNCH(false)
+  }
+#undef H2S_PEAK_LAUNCH
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_peak_finish, dim3(P.nframes), dim3(256), 0, s, partial, T);
   return hipGetLastError();
+}
+
+// h2s_peak_feed: the IIR over caller-supplied statistics.  One block
+void __global__ __launch_bounds__(64) k_peak_curves(double2* fstat, int n, const PeakModel M, PeakState* st,
+                                                    CurveConsts* out) {
+  peak_curves_body(fstat, n, M, st, out);
 }
 
 hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out,

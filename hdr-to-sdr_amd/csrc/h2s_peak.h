@@ -6,9 +6,11 @@
 // peak in the tile kernel's folded form (CurveConsts).
 //
 // One definition serves the host (the static curve of h2s_set_params) and the
-// device (k_peak_frame / k_peak_curves in h2s_kernels.hip: h2s_process with
-// peak_detect queues statistics -> curves -> conversion on its stream with no
-// host round trip), so the two cannot drift apart.  The oracle's statement is
+// device (k_peak_stats* + k_peak_finish in h2s_kernels.hip: h2s_process with
+// peak_detect queues the statistics, then the per-frame fold with the IIR and
+// curve records in its last block, then the conversion, on its stream with no
+// host round trip; k_peak_curves serves h2s_peak_feed), so the two cannot
+// drift apart.  The oracle's statement is
 // oracle/h2s_oracle.c (PeakState, resolve).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -27,6 +29,7 @@ struct PeakModel {
   double knee_off, contrast, tm_param;
   double static_peak;                 // the clamp's top: the metadata / default peak (units of 100 nits)
   double smoothing, scene_low, scene_high, percentile, min_peak;  // vf_libplacebo options (min_peak x 100 nits)
+  double iir_a;                       // the IIR coefficient 1 - exp(-1 / smoothing) (1: no smoothing), host-made
   double npx;                         // pixels per frame
   int nblocks;                        // partial records per frame
   int pct;                            // percentile < 100: histograms present
@@ -37,6 +40,20 @@ struct PeakModel {
 struct PeakState {
   double max, avg, peak;
   long long frames;
+};
+
+// The buffers of a statistics launch (k_peak_stats* then k_peak_finish, in
+// h2s_kernels.hip).  The histograms and the counter are zero on entry and are
+// left zero (h2s_api.hip clears them once, at allocation).
+struct PeakTail {
+  PeakModel M;
+  double2* fstat;      // nframes: the frames' (measurement, average)
+  unsigned* hist;      // nframes x PEAK_BINS (M.pct)
+  unsigned* done;      // one counter (frames folded)
+  PeakState* st;       // null: the statistics only (h2s_peak_stats)
+  CurveConsts* out;    // nframes curve records, or null
+  int nframes;
+  int form;            // PQ streaming form: 0 = 8-pixel row chunks, 1 = 2 x 8 chunks (test hook A/B)
 };
 
 __host__ __device__ inline double hd_pq_encode(double y) {
@@ -198,14 +215,14 @@ __host__ __device__ inline double peak_of(const PeakModel& m, double max_pq) {
 
 // one frame into the smoothing state (max, avg, frames; the caller sets
 // .peak = peak_of(m, .max) for the last frame).  IIR with coefficient
-// 1 - exp(-1 / smoothing_period) on the PQ-domain frame max and average; a
+// m.iir_a = 1 - exp(-1 / smoothing_period) on the PQ-domain frame max and average; a
 // scene change (frame-average jump of scene_low .. scene_high % PQ) bypasses
 // it progressively (smoothstep); negative thresholds turn that off
 __host__ __device__ inline void peak_iir_step(PeakState* s, const PeakModel& m, double fmax, double favg) {
   if (s->frames == 0) {
     s->max = fmax, s->avg = favg;
   } else {
-    const double a = m.smoothing > 0.0 ? 1.0 - exp(-1.0 / m.smoothing) : 1.0;
+    const double a = m.iir_a;
     const double d = fabs(favg - s->avg) * 100.0;
     double t = 0.0;
     if (m.scene_low >= 0.0 && m.scene_high >= 0.0)

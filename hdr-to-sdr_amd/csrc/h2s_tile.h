@@ -124,15 +124,29 @@ __device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log
 }
 
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
-// (build_pqi_table): the segment is the float's exponent and top two mantissa
-// bits, t the remaining 21 mantissa bits as [0, 1/4); clamped to the table's
-// octaves 2^-40 .. 2^14
+// (build_pqi_table): the segment is the float's exponent and top three
+// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); octaves
+// 2^-34 .. 2^14 (clamped at the top: the IPT form caps its input at 1e6 npl).
+// Eight segments per octave, not four: the LMS encode error the decode
+// amplifies (x ~11-45 through the EOTF's slope) drops from ~1e-6 to the
+// float32 floor, and the libplacebo branch's rgba8 download flips 7x less
+// often (scripts/c3_table_flips.py).  Below 2^-34 (3e-7 nits: black) the
+// direct form, ((c1 + c2 y^m1) / (1 + c3 y^m1))^m2 on v_log / v_exp, in a
+// divergent branch only the lanes there take (black frames' areas: whole waves)
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
-  const unsigned b = __builtin_bit_cast(unsigned, y) & 0x7FFFFFFFu;
-  const int sg = min(max((int)(b >> 21) - ((127 + PQI_OCT0) << 2), 0), PQI_NSEG - 1);
-  const float t = __builtin_bit_cast(float, (b & 0x1FFFFFu) | 0x3F800000u) - 1.0f;
+  // y <= 0 (an LMS row of a saturated colour can go negative) encodes as 0,
+  // as the oracle's max(y, 0): the bit pattern clamps to +0, the direct form
+  const unsigned b = (unsigned)max((int)__builtin_bit_cast(unsigned, y), 0);
+  const int sr = (int)(b >> 20) - ((127 + PQI_OCT0) << 3);
+  const int sg = min(max(sr, 0), PQI_NSEG - 1);
+  const float t = __builtin_bit_cast(float, (b & 0xFFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
-  return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
+  float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
+  if (sr < 0) {
+    const float ym = fexp2(flog2(__builtin_bit_cast(float, b)) * PQ_M1);   // y = 0: log2 -> -inf, ym = 0
+    v = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
+  }
+  return v;
 }
 
 // S1 transfer to linear (units of npl), specialised
@@ -653,6 +667,10 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   }
   if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
+  if (F.eq_ident) {   // launch-uniform: the identity table is not staged
+    if constexpr (EQM) return (uint16_t)__builtin_bit_cast(unsigned, o.x + 8388608.0f);
+    return (uint16_t)(int)o.x;
+  }
   if constexpr (EQM) {
     // o.x = the luma quantiser input less 0.5 (the lattice records carry no
     // +0.5): adding 2^23 rounds it to the nearest integer in the mantissa's
@@ -980,8 +998,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   }
   // codes at the output depth: shift, or bit replication (h2s_expand;
   // rep_rs = 8 - shift, or 31 for a plain shift: the 8-bit code >> 31 = 0)
-  if (t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
-  for (int i = t + 256; i < F.eq_n; i += 256) {  // native 10/12-bit tables
+  if (!F.eq_ident && t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
+  for (int i = t + 256; !F.eq_ident && i < F.eq_n; i += 256) {  // native 10/12-bit tables
     const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
     eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
   }
