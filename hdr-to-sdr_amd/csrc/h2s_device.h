@@ -91,6 +91,10 @@ struct KParams {
   // dynamic peak detection (one frame per launch): the frame's curve record,
   // written on the device by k_peak_curves; null: the constants above
   const CurveConsts* cv;
+  // near-tie exact pass (k_process LIST form): the quads k_tile<..., LP = 2>
+  // listed; cv then points at the launch's per-frame records (or is null)
+  const unsigned* nt_list;
+  const unsigned* nt_count;
 };
 
 constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
@@ -176,6 +180,13 @@ struct FastParams : CurveConsts {
   float lp_qs_f, lp_qo;
   int lp_dith;
   unsigned in_mask2;
+  // near-tie instances (k_tile<..., LP = 2>, H2S_OPT_LP_EXACT 1): the rgba8
+  // tie window's scale (qs NT_D / 2.4) and the list of quads (index
+  // (f ch + cy) cw + cx) whose download may round the other way, appended at
+  // nt_list[atomicAdd(nt_count)] for k_process's exact pass
+  float nt_scale;
+  unsigned* nt_list;
+  unsigned* nt_count;
   float ipt_r2l[9], ipt_l2r[9];
   const float4* pqi_tab;
   // libplacebo branch with the LUT off (k_tile<..., LP = 1>): libplacebo's own
@@ -187,6 +198,7 @@ struct FastParams : CurveConsts {
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
+  float stride_r;                              // 12 (the cell-major A/B layout: 128)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)
   int og, ob, cr, cg, cb, c111;                // corner byte offsets
   const float* lut_yuv;                        // 12-byte records (Y', Cb', Cr')

@@ -57,6 +57,10 @@
 namespace h2s {
 
 typedef float f3 __attribute__((ext_vector_type(3)));
+#ifndef H2S_LP_BLEND_FUSED
+#define H2S_LP_BLEND_FUSED 0   // 1: the libplacebo blend contracted into FMAs (pre-round-5 code, A/B)
+#endif
+
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
@@ -230,12 +234,14 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // table, L'M'S' += I' - I decoded through the EOTF table), as the oracle's
 // tone_ipt.
 // DARK: the dark re-run (px_chain): every EOTF-table read takes its first
-// segment exactly (pq_z_dark) instead of the NaN staged there.  luma: the
-// desaturation's luma (DESAT instances), the CPU chain's free NaN probe
+// segment exactly (pq_z_dark) instead of the mark staged there.  luma: the
+// desaturation's luma (DESAT instances), the CPU chain's free dark probe.
+// kap (LP == 2, the near-tie instances): per output channel c, the IPT rows'
+// conditioning sum_k |l2r[c][k] LMS_k| / |c| (px_chain's rgba8 tie window)
 template <int TRC, int TM, int DESAT, int LP, bool DARK = false>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
                                      const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s,
-                                     float hable_kb, float& luma_out) {
+                                     float hable_kb, float& luma_out, float (&kap)[3]) {
   auto pz = [&](float u) { return DARK ? pq_z_dark(pq_lds, u, F.log2_pq_scale) : pq_z(pq_lds, u); };
   if (LP && TM >= 4 && TM <= 6) {
     // libplacebo's reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = the
@@ -337,6 +343,13 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
       g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
       b = F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2;
+      if constexpr (LP == 2) {
+        const float* A = F.ipt_l2r;
+        const float a0 = fabsf(l0), a1 = fabsf(l1), a2 = fabsf(l2);
+        kap[0] = fmaf(fabsf(A[0]), a0, fmaf(fabsf(A[1]), a1, fabsf(A[2]) * a2)) * frcp(fabsf(r));
+        kap[1] = fmaf(fabsf(A[3]), a0, fmaf(fabsf(A[4]), a1, fabsf(A[5]) * a2)) * frcp(fabsf(g));
+        kap[2] = fmaf(fabsf(A[6]), a0, fmaf(fabsf(A[7]), a1, fabsf(A[8]) * a2)) * frcp(fabsf(b));
+      }
       return;
     }
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
@@ -420,6 +433,7 @@ __device__ __forceinline__ float lut_s(const FastParams& F, float x) {
 struct StepK {
   float a_rv, a_gv, a_gu, a_bu;   // chroma terms of E, x ESC
   float stride_g, stride_b;       // lattice byte strides (as floats)
+  float stride_r;
   int og, ob, ocr, ocg, ocb;      // corner byte offsets
   float log2_nm1, x_max;
   float hable_kb;                 // F.hable_kb (Hable instances)
@@ -437,7 +451,8 @@ template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv, float qoff, float ydq) {
+                                             long long di, float& oyv, float& ozv, float qoff, float ydq,
+                                             bool& tie) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
   // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
@@ -463,8 +478,8 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   // marked channel back to the curve's output (k = curve(sig) / sig)
   constexpr bool S1P = TRC == 0 && (LP || !(DESAT && TM <= 6));
   const float s1probe = S1P ? (r + gg) + bl : 0.0f;
-  float luma = 0.0f;
-  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
+  float luma = 0.0f, kap[3] = {0.0f, 0.0f, 0.0f};
+  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma, kap);
   // The EOTF table's first segment is marked wherever it is read (S1 on PQ
   // input; the libplacebo branch's IPT decode and curve reads): a value that
   // reached it is huge (> DARK_MARK) in S1's output or the tone map's.  The
@@ -483,7 +498,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     }
     if (__builtin_amdgcn_ballot_w64(!(probe <= DARK_MARK))) {   // (NaN / inf from a marked value too)
       const bool safe2 = to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r, gg, bl);
-      tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
+      tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma, kap);
     }
   }
   if (DBG == 2) dput(r, gg, bl);
@@ -512,11 +527,20 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       // lut3d's 8-bit coordinate (q / 255) (N-1) in its own operation order:
       // q = 255 lands on N-1 exactly (fract 0: the corners past the lattice
       // edge get weight 0 and read in-bounds records or the buffer's zero fill)
-      auto q8 = [&](float x) -> float {
+      // LP == 2 (near-tie instances): a code whose quantiser input lies
+      // within the window of an integer may round the other way in the
+      // reference's double-precision IPT form; the window is the stage-3
+      // error bound NT_D x (255 x BT.1886 + 255 b) x kap / 2.4 (the IPT rows'
+      // conditioning through the encode's slope) at the quantiser's scale
+      // (F.nt_scale = qs NT_D / 2.4), and such a pixel's quad is listed for
+      // k_process's exact pass (steps())
+      auto q8 = [&](float x, float kp) -> float {
         const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
+        const float tq = fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
+        if constexpr (LP == 2) tie = tie || fabsf(tq - __builtin_rintf(tq)) < (e + F.lp_k2) * kp * F.nt_scale;
+        return floorf(tq);
       };
-      const float qr = q8(r), qg = q8(gg), qb = q8(bl);
+      const float qr = q8(r, kap[0]), qg = q8(gg, kap[1]), qb = q8(bl, kap[2]);
       if (DBG == 3) {
         auto ev = [&](float x) {
           const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
@@ -551,7 +575,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     // misaligned record (N = 177: 45 of 3072 samples of a uniform frame)
     asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
     const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-    const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * 12.0f));
+    const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * K.stride_r));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
     // fractions: the 4 low mantissa bits of each fraction carry its axis a
     // (bits 3:2 and 1:0 both = a; r 0, g 1, b 2; a change of <= 2^-19
@@ -594,9 +618,15 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       if constexpr (LP) {
         // lut3d's 8-bit path truncates its output to 8 bits: the blend in
         // the oracle's (vf_lut3d C) order, products and sums each rounded (no
-        // FMA), so that a blend on an integer boundary truncates alike
+        // FMA), so that a blend on an integer boundary truncates alike.
+        // (__fmul_rn / __fadd_rn are plain operators in HIP and were being
+        // contracted into v_fmac under hipcc's default fp-contract=fast until
+        // round 5: the pragma is what keeps the products rounded)
         auto ch = [&](float a, float b, float c, float d) {
-          return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(w0, a), __fmul_rn(w1, b)), __fmul_rn(w2, c)), __fmul_rn(w3, d));
+#if !H2S_LP_BLEND_FUSED
+#pragma clang fp contract(off)
+#endif
+          return ((w0 * a + w1 * b) + w2 * c) + w3 * d;
         };
         return f3{ch(c0.x, c1.x, c2.x, c3.x), ch(c0.y, c1.y, c2.y, c3.y), ch(c0.z, c1.z, c2.z, c3.z)};
       }
@@ -1041,7 +1071,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
-  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
+  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, in_vgpr(F.stride_r), og, ob, ocr, ocg, ocb, log2_nm1, x_max,
                 TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab};
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
@@ -1077,9 +1107,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
                                ? (long long)(g.py0 + yl + 8 * (s >> 1)) * F.dbg_w + g.px0 + xl + 8 * (s & 1)
                                : -1;
       float oyv, ozv;
+      bool tie = false;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
+          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq, tie);
+      if constexpr (LP == 2) {
+        // a pixel near an rgba8 tie lists its quad (the 2x2 pixels of one
+        // output chroma sample) for the exact pass: one atomic per wave
+        // (a ballot's popcount), the quad leaders' slots by mbcnt
+        const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
+        const bool lead = quad_sum(tie ? 1.0f : 0.0f) > 0.0f && (lane & 3) == 0 && px < F.W && py < F.H;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(lead);
+        if (m) {
+          unsigned base = 0;
+          if (lane == 0) base = atomicAdd(F.nt_count, (unsigned)__builtin_popcountll(m));
+          base = __builtin_amdgcn_readfirstlane(base);
+          const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          if (lead)
+            F.nt_list[base + below] = ((unsigned)g.f * (unsigned)F.ch + (unsigned)(py >> 1)) * (unsigned)F.cw + (unsigned)(px >> 1);
+        }
+      }
       if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
@@ -1150,6 +1197,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   X(0, 8, 0, 0)       \
   X(0, 7, 0, 1)       \
   X(0, 8, 0, 1)       \
+  X(0, 7, 0, 2)       \
+  X(0, 8, 0, 2)       \
   X(0, 4, 0, 1)       \
   X(0, 5, 0, 1)       \
   X(0, 6, 0, 1)       \
@@ -1166,6 +1215,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   X(1, 8, 0, 0)       \
   X(1, 7, 0, 1)       \
   X(1, 8, 0, 1)       \
+  X(1, 7, 0, 2)       \
+  X(1, 8, 0, 2)       \
   X(1, 4, 0, 1)       \
   X(1, 5, 0, 1)       \
   X(1, 6, 0, 1)

@@ -12,7 +12,7 @@ export H2S_FLOAT_REPORT=$OUT/float_report.jsonl
 export H2S_PARITY_REPORT=$OUT/parity_report.jsonl
 rm -f "$H2S_FLOAT_REPORT" "$H2S_PARITY_REPORT"
 if [ "${SKIP_SUITE:-0}" != 1 ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=40 -q --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=60 -q --timeout 300 --timeout-method thread \
     ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?
   tail -5 "$OUT/pytest_gpu.log"
