@@ -30,7 +30,6 @@ hipError_t launch_yuv8_rgb24(const uint8_t* yp, long long yls, const uint8_t* up
                              long long yuv_fp, int w, int h, uint8_t* rgb, long long rls, long long rgb_fp,
                              const uint8_t* glut, int nframes, hipStream_t s);
 hipError_t launch_peak_stats(const KParams& P, float2* partial, const PeakTail& T, hipStream_t s);
-hipError_t launch_neartie_fix(const KParams& P, bool out8, hipStream_t s);
 hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out,
                               hipStream_t s);
 }  // namespace h2s
@@ -55,10 +54,7 @@ struct h2s_ctx {
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   bool fast_enabled = true;
-  int lp_exact = 0;       // H2S_OPT_LP_EXACT: 0 off, 1 near-tie exact pass, 2 generic kernel
-  double nt_d = 6e-6;     // the near-tie window's stage-3 bound (H2S_OPT_TEST_NT_WINDOW)
-  unsigned* d_nt = nullptr;   // [0] the listed-quad count, [1..] the list
-  size_t nt_cap = 0;
+  bool lp_exact = false;  // H2S_OPT_LP_EXACT
   int peak_form = 0;      // H2S_OPT_TEST_PEAK_FORM (private A/B hook)
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
@@ -96,7 +92,7 @@ struct h2s_ctx {
   // streams they went to: set_params / set_lut wait for exactly these (no
   // device-wide synchronisation), then recycle them
   std::vector<hipEvent_t> pend, ev_free;
-  hipEvent_t chr_ev = nullptr;   // after the last BICUBIC two-pass or near-tie launch (d_chr / d_nt in use)
+  hipEvent_t chr_ev = nullptr;   // after the last BICUBIC two-pass launch (d_chr scratch in use)
   // set_params / set_lut copy and (re)allocate on this non-blocking stream
   // (stream-ordered hipMallocAsync / hipFreeAsync for the lattices): no
   // null-stream copy or hipFree, which would wait for the whole device
@@ -673,7 +669,6 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_prev) hipFree(c->d_prev);
   if (c->d_stats) hipFree(c->d_stats);
-  if (c->d_nt) hipFree(c->d_nt);
   if (c->d_fstat) hipFree(c->d_fstat);
   if (c->d_curve) hipFree(c->d_curve);
   if (c->d_pk) hipFree(c->d_pk);
@@ -1052,14 +1047,6 @@ static hipError_t launch_two_pass_frames(const h2s_ctx* c, const KParams& k, boo
   return hipSuccess;
 }
 
-// H2S_OPT_LP_EXACT 1 runs the tile kernel's near-tie instances plus the exact
-// pass where they exist: BT.2390 / spline on the IPT form with the LUT on and
-// box chroma (the other libplacebo forms take the generic kernel)
-static bool neartie_ok(const h2s_ctx* c, const KParams& k) {
-  return k.pipe == h2s::PIPE_LIBPLACEBO && k.lp_ipt && k.lut_enabled && (k.tonemap == 7 || k.tonemap == 8) &&
-         c->params.chroma_filter != H2S_CHROMA_BICUBIC;
-}
-
 static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bool vec, bool out8, int nframes,
                                hipStream_t s, const h2s::CurveConsts* cvf, bool tail, int dbg, float* dbg_out,
                                float2* chr444);
@@ -1136,26 +1123,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
   F.chr_w = k.W;
   F.inv_c56 = 1.0f / F.c56;
   const int desat = !k.desat_on ? 0 : (k.lr == 1.0f && k.lg == 1.0f && k.lb == 1.0f ? 2 : 1);
-  // near-tie exact pass (H2S_OPT_LP_EXACT 1): the tile kernel lists the quads
-  // whose rgba8 download may round the other way (a zeroed count, the list
-  // sized for every quad of the launch), k_process recomputes them exactly
-  const bool nt = c->lp_exact == 1 && !dbg && !chr444 && neartie_ok(c, k);
-  if (nt) {
-    F.nt_count = c->d_nt;
-    F.nt_list = c->d_nt + 1;
-    F.nt_scale = (float)((double)F.lp_qs_f * c->nt_d / 2.4);
-    hipError_t e = hipMemsetAsync(c->d_nt, 0, sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
-  }
-  int lp = k.pipe == h2s::PIPE_LIBPLACEBO ? (nt ? 2 : 1) : 0;
-  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, lp, s, dbg);
-  if (e == hipSuccess && nt) {
-    KParams kx = k;
-    kx.nt_list = c->d_nt + 1;
-    kx.nt_count = c->d_nt;
-    kx.cv = cvf;
-    e = h2s::launch_neartie_fix(kx, out8, s);
-  }
+  hipError_t e = h2s::launch_fast(F, k.transfer, k.tonemap, desat, k.pipe == h2s::PIPE_LIBPLACEBO ? 1 : 0, s, dbg);
   if (e != hipSuccess || w64 == k.W || !tail || dbg) return e;
   return launch_tail(k, nframes, vec, out8, s, tw);
 }
@@ -1169,7 +1137,7 @@ static hipError_t launch_chain(const h2s_ctx* c, const KParams& k, bool fast, bo
 static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   const h2s_params& p = c->params;
   if (!c->fast_enabled || !h2s::fast_supported(k.tonemap)) return false;
-  if (c->lp_exact && k.pipe == h2s::PIPE_LIBPLACEBO && !(c->lp_exact == 1 && neartie_ok(c, k))) return false;
+  if (c->lp_exact && k.pipe == h2s::PIPE_LIBPLACEBO) return false;
   // the LUT off runs on the tile kernel for the libplacebo branch only (the
   // CPU chain's legacy closed form stays on the generic kernel)
   if (!k.lut_enabled && k.pipe != h2s::PIPE_LIBPLACEBO) return false;
@@ -1561,18 +1529,12 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   const int path = choose_path(c, k, &din, &dout, out8);
   const bool fast = path == H2S_PATH_TILE || path == H2S_PATH_TILE_TAIL;
   if (fast && k.lut_enabled && (rc = ensure_lut_yuv(c, k, s))) return rc;
-  // BICUBIC chroma (generic two-pass, or k_tile pass 1) uses the context
-  // scratch d_chr; the near-tie exact pass (H2S_OPT_LP_EXACT 1) its quad list
+  // BICUBIC chroma (generic two-pass, or k_tile pass 1) uses the context scratch
   const bool two_pass = c->params.chroma_filter == H2S_CHROMA_BICUBIC;
-  const bool nt_list = fast && c->lp_exact == 1 && neartie_ok(c, k);
-  if (nt_list && (rc = ensure_dev(c, (void**)&c->d_nt, &c->nt_cap,
-                                  (1 + (size_t)nframes * (size_t)k.cw * (size_t)k.ch) * sizeof(unsigned),
-                                  "near-tie quad list")))
-    return rc;
-  if (two_pass || nt_list) {
-    if (two_pass && (rc = ensure_chr(c, k))) return rc;
-    // one context scratch for every such launch: a launch on another stream
-    // waits until the previous one has finished with it
+  if (two_pass) {
+    if ((rc = ensure_chr(c, k))) return rc;
+    // one context scratch (d_chr) for every two-pass launch: a launch on
+    // another stream waits until the previous one has finished with it
     if (!c->chr_ev) {
       hipError_t e = hipEventCreateWithFlags(&c->chr_ev, hipEventDisableTiming);
       if (e != hipSuccess) {
@@ -1623,7 +1585,7 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
     e = copy_frames(out, &dout, nframes, s);
     if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "device->host copy"));
   }
-  if (two_pass || nt_list) {
+  if (two_pass) {
     if ((e = hipEventRecord(c->chr_ev, s)) != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "two-pass event"));
     c->chr_pending = true;
   }
@@ -1703,12 +1665,7 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
       c->serial_host = value != 0;
       return 0;
     case H2S_OPT_LP_EXACT:
-      if (value < 0 || value > 2) return fail(c, H2S_E_INVALID_ARG, "H2S_OPT_LP_EXACT takes 0, 1 or 2");
-      c->lp_exact = (int)value;
-      return 0;
-    case H2S_OPT_TEST_NT_WINDOW:
-      if (value <= 0) return fail(c, H2S_E_INVALID_ARG, "near-tie window must be positive (units of 1e-9)");
-      c->nt_d = (double)value * 1e-9;
+      c->lp_exact = value != 0;
       return 0;
     case H2S_OPT_TEST_FAIL_AFTER_LAUNCH:
       c->fail_after_launch = value != 0;

@@ -91,10 +91,6 @@ struct KParams {
   // dynamic peak detection (one frame per launch): the frame's curve record,
   // written on the device by k_peak_curves; null: the constants above
   const CurveConsts* cv;
-  // near-tie exact pass (k_process LIST form): the quads k_tile<..., LP = 2>
-  // listed; cv then points at the launch's per-frame records (or is null)
-  const unsigned* nt_list;
-  const unsigned* nt_count;
 };
 
 constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
@@ -180,13 +176,6 @@ struct FastParams : CurveConsts {
   float lp_qs_f, lp_qo;
   int lp_dith;
   unsigned in_mask2;
-  // near-tie instances (k_tile<..., LP = 2>, H2S_OPT_LP_EXACT 1): the rgba8
-  // tie window's scale (qs NT_D / 2.4) and the list of quads (index
-  // (f ch + cy) cw + cx) whose download may round the other way, appended at
-  // nt_list[atomicAdd(nt_count)] for k_process's exact pass
-  float nt_scale;
-  unsigned* nt_list;
-  unsigned* nt_count;
   float ipt_r2l[9], ipt_l2r[9];
   const float4* pqi_tab;
   // libplacebo branch with the LUT off (k_tile<..., LP = 1>): libplacebo's own

@@ -8,7 +8,6 @@ namespace h2s {
 
 H2S_TILE_INSTANCE(0, 0)
 H2S_TILE_EXTERN(0, 1)   // h2s_fast_lp.hip
-H2S_TILE_EXTERN(0, 2)   // h2s_fast_lpx.hip
 H2S_TILE_EXTERN(1, 0)
 H2S_TILE_EXTERN(1, 1)
 H2S_TILE_EXTERN(2, 0)
@@ -44,9 +43,6 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
-#ifndef H2S_CELL_LAYOUT
-#define H2S_CELL_LAYOUT 0
-#endif
 #if H2S_CELL_LAYOUT
 // A/B build only (the brick-layout candidate in its
 // zero-address-cost form): the lattice stored cell-major, each cell's eight
@@ -75,8 +71,7 @@ __global__ void k_build_lut_cell(const float* lin, float* cell, int n) {
 #endif
 
 // desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma (vf_tonemap's; the
-// libplacebo curves have none).  lp: the libplacebo branch (every operator);
-// 2: its near-tie instances (BT.2390 / spline, product kernel only).
+// libplacebo curves have none).  lp: the libplacebo branch (every operator).
 // dbg: 0 = the
 // product kernel; 1..5 = its debug instance for that h2s_stage (F.dbg set)
 hipError_t launch_fast(const FastParams& F0, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
@@ -105,7 +100,6 @@ hipError_t launch_fast(const FastParams& F0, int trc, int tm, int desat, int lp,
   if (tm == 7 || tm == 8 || lp) desat = 0;
 #define H2S_DISPATCH(D) \
   return lp ? launch_tile<D, 1>(F, trc, tm, desat, grid, lds, s) : launch_tile<D, 0>(F, trc, tm, desat, grid, lds, s)
-  if (lp == 2) return dbg == 0 ? launch_tile<0, 2>(F, trc, tm, desat, grid, lds, s) : hipErrorInvalidValue;
   switch (dbg) {
     case 0: H2S_DISPATCH(0);
     case 1: H2S_DISPATCH(1);

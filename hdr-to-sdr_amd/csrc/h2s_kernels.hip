@@ -32,11 +32,7 @@ __device__ __forceinline__ int ld16(const uint8_t* row, int x) {
 // C444: BICUBIC chroma (two-pass path): store every pixel's (Cb, Cr) into
 // P.chr444 (frame 0 of the launch, W x H) instead of the 2x2 mean; the
 // chroma planes are then written by k_chroma_bicubic
-// LIST (the near-tie exact pass, QPT 1): the work items are the quads
-// k_tile<..., LP = 2> listed (P0.nt_list[0 .. *P0.nt_count), index
-// (f ch + cy) cw + cx), a grid-stride loop over them; P0.cv, if set, holds the
-// launch's per-frame curve records
-template <int QPT, bool VEC, bool OUT8, bool C444 = false, bool DYN = false, bool LIST = false>
+template <int QPT, bool VEC, bool OUT8, bool C444 = false, bool DYN = false>
 __global__ __launch_bounds__(256) void k_process(const KParams P0) {
   auto body = [&](const KParams& P, const int f, const int cy, const int cx0) {
   const int cw = P.cw, ch = P.ch;
@@ -199,21 +195,6 @@ __global__ __launch_bounds__(256) void k_process(const KParams P0) {
     }
   }
   };
-  if constexpr (LIST) {
-    static_assert(QPT == 1 && !VEC && !C444 && !DYN, "the exact pass takes single quads");
-    const unsigned n = *P0.nt_count, per = (unsigned)P0.cw * (unsigned)P0.ch;
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-      const unsigned qi = P0.nt_list[i], f = qi / per, rem = qi - f * per, cy = rem / (unsigned)P0.cw;
-      if (P0.cv) {
-        KParams P = P0;
-        apply_curve(P, P0.cv[f]);
-        body(P, (int)f, (int)cy, (int)(rem - cy * (unsigned)P0.cw));
-      } else {
-        body(P0, (int)f, (int)cy, (int)(rem - cy * (unsigned)P0.cw));
-      }
-    }
-    return;
-  }
   // DYN (dynamic peak detection, one frame per launch): the frame's curve
   // constants come from the record the peak launches wrote on the device
   // (P0.cv), not from the launch parameters
@@ -227,14 +208,6 @@ __global__ __launch_bounds__(256) void k_process(const KParams P0) {
   body(P, (int)(t / P.ch), (int)(t % P.ch), (gx + P.gx0) * QPT);
 }
 
-// the near-tie exact pass over the quads k_tile<..., LP = 2> listed (the
-// count stays on the device: a fixed grid walks the list)
-hipError_t launch_neartie_fix(const KParams& P, bool out8, hipStream_t s) {
-  const dim3 grid(2048), block(256);
-  if (out8) hipLaunchKernelGGL((k_process<1, false, true, false, false, true>), grid, block, 0, s, P);
-  else hipLaunchKernelGGL((k_process<1, false, false, false, false, true>), grid, block, 0, s, P);
-  return hipGetLastError();
-}
 
 // Debug/parity kernel: float RGB of frame 0 after stage STAGE, one thread per
 // pixel, generic (unvectorised) sample access.

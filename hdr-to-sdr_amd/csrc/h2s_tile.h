@@ -57,6 +57,12 @@
 namespace h2s {
 
 typedef float f3 __attribute__((ext_vector_type(3)));
+#ifndef H2S_PQI_DIRECT
+#define H2S_PQI_DIRECT 1   // 0: PQ encodes below the table's first octave clamp to it (A/B)
+#endif
+#ifndef H2S_CELL_LAYOUT
+#define H2S_CELL_LAYOUT 0   // 1: the cell-major lattice A/B (h2s_fast.hip): the r stride from FastParams
+#endif
 #ifndef H2S_LP_BLEND_FUSED
 #define H2S_LP_BLEND_FUSED 0   // 1: the libplacebo blend contracted into FMAs (pre-round-5 code, A/B)
 #endif
@@ -146,7 +152,7 @@ __device__ __forceinline__ float pqi(const float4* tab, float y) {
   const float t = __builtin_bit_cast(float, (b & 0xFFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
   float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
-  if (sr < 0) {
+  if (H2S_PQI_DIRECT && sr < 0) {
     const float ym = fexp2(flog2(__builtin_bit_cast(float, b)) * PQ_M1);   // y = 0: log2 -> -inf, ym = 0
     v = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
   }
@@ -235,13 +241,11 @@ __device__ __forceinline__ bool to_linear(const FastParams& F, const float4* pq_
 // tone_ipt.
 // DARK: the dark re-run (px_chain): every EOTF-table read takes its first
 // segment exactly (pq_z_dark) instead of the mark staged there.  luma: the
-// desaturation's luma (DESAT instances), the CPU chain's free dark probe.
-// kap (LP == 2, the near-tie instances): per output channel c, the IPT rows'
-// conditioning sum_k |l2r[c][k] LMS_k| / |c| (px_chain's rgba8 tie window)
+// desaturation's luma (DESAT instances), the CPU chain's free dark probe
 template <int TRC, int TM, int DESAT, int LP, bool DARK = false>
 __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, const float4* pq_lds,
                                      const float4* pqi_lds, float& r, float& g, float& b, bool safe, float emax_s,
-                                     float hable_kb, float& luma_out, float (&kap)[3]) {
+                                     float hable_kb, float& luma_out) {
   auto pz = [&](float u) { return DARK ? pq_z_dark(pq_lds, u, F.log2_pq_scale) : pq_z(pq_lds, u); };
   if (LP && TM >= 4 && TM <= 6) {
     // libplacebo's reinhard / hable / mobius (scaling PL_HDR_NORM: 1 = the
@@ -343,13 +347,6 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
       g = F.ipt_l2r[3] * l0 + F.ipt_l2r[4] * l1 + F.ipt_l2r[5] * l2;
       b = F.ipt_l2r[6] * l0 + F.ipt_l2r[7] * l1 + F.ipt_l2r[8] * l2;
-      if constexpr (LP == 2) {
-        const float* A = F.ipt_l2r;
-        const float a0 = fabsf(l0), a1 = fabsf(l1), a2 = fabsf(l2);
-        kap[0] = fmaf(fabsf(A[0]), a0, fmaf(fabsf(A[1]), a1, fabsf(A[2]) * a2)) * frcp(fabsf(r));
-        kap[1] = fmaf(fabsf(A[3]), a0, fmaf(fabsf(A[4]), a1, fabsf(A[5]) * a2)) * frcp(fabsf(g));
-        kap[2] = fmaf(fabsf(A[6]), a0, fmaf(fabsf(A[7]), a1, fabsf(A[8]) * a2)) * frcp(fabsf(b));
-      }
       return;
     }
     const float sig = fmaxf(__builtin_fmaxf(__builtin_fmaxf(r, g), b), 1e-6f);
@@ -451,8 +448,7 @@ template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
                                              const float4* pqi_lds, const uint16_t* eq_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv, float qoff, float ydq,
-                                             bool& tie) {
+                                             long long di, float& oyv, float& ozv, float qoff, float ydq) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
   // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
@@ -478,8 +474,8 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   // marked channel back to the curve's output (k = curve(sig) / sig)
   constexpr bool S1P = TRC == 0 && (LP || !(DESAT && TM <= 6));
   const float s1probe = S1P ? (r + gg) + bl : 0.0f;
-  float luma = 0.0f, kap[3] = {0.0f, 0.0f, 0.0f};
-  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma, kap);
+  float luma = 0.0f;
+  tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
   // The EOTF table's first segment is marked wherever it is read (S1 on PQ
   // input; the libplacebo branch's IPT decode and curve reads): a value that
   // reached it is huge (> DARK_MARK) in S1's output or the tone map's.  The
@@ -498,7 +494,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     }
     if (__builtin_amdgcn_ballot_w64(!(probe <= DARK_MARK))) {   // (NaN / inf from a marked value too)
       const bool safe2 = to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r, gg, bl);
-      tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma, kap);
+      tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
     }
   }
   if (DBG == 2) dput(r, gg, bl);
@@ -527,20 +523,11 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       // lut3d's 8-bit coordinate (q / 255) (N-1) in its own operation order:
       // q = 255 lands on N-1 exactly (fract 0: the corners past the lattice
       // edge get weight 0 and read in-bounds records or the buffer's zero fill)
-      // LP == 2 (near-tie instances): a code whose quantiser input lies
-      // within the window of an integer may round the other way in the
-      // reference's double-precision IPT form; the window is the stage-3
-      // error bound NT_D x (255 x BT.1886 + 255 b) x kap / 2.4 (the IPT rows'
-      // conditioning through the encode's slope) at the quantiser's scale
-      // (F.nt_scale = qs NT_D / 2.4), and such a pixel's quad is listed for
-      // k_process's exact pass (steps())
-      auto q8 = [&](float x, float kp) -> float {
+      auto q8 = [&](float x) -> float {
         const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        const float tq = fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
-        if constexpr (LP == 2) tie = tie || fabsf(tq - __builtin_rintf(tq)) < (e + F.lp_k2) * kp * F.nt_scale;
-        return floorf(tq);
+        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
       };
-      const float qr = q8(r, kap[0]), qg = q8(gg, kap[1]), qb = q8(bl, kap[2]);
+      const float qr = q8(r), qg = q8(gg), qb = q8(bl);
       if (DBG == 3) {
         auto ev = [&](float x) {
           const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
@@ -575,7 +562,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     // misaligned record (N = 177: 45 of 3072 samples of a uniform frame)
     asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
     const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-    const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * K.stride_r));
+    const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * (H2S_CELL_LAYOUT ? K.stride_r : 12.0f)));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
     // fractions: the 4 low mantissa bits of each fraction carry its axis a
     // (bits 3:2 and 1:0 both = a; r 0, g 1, b 2; a change of <= 2^-19
@@ -994,7 +981,11 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 #ifndef H2S_TILE_WPE
 #define H2S_TILE_WPE 5
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WPE))) void k_tile(const FastParams F) {
+#ifndef H2S_TILE_WPE_LP
+#define H2S_TILE_WPE_LP H2S_TILE_WPE   // the libplacebo instances (A/B)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TILE_WPE_LP : H2S_TILE_WPE))) void k_tile(
+    const FastParams F) {
   constexpr int YST = row_stride<LP>(), HST = YST;
   __shared__ float yin[TBH * YST];             // luma samples x ys; output codes overwrite them in place
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
@@ -1107,26 +1098,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
                                ? (long long)(g.py0 + yl + 8 * (s >> 1)) * F.dbg_w + g.px0 + xl + 8 * (s & 1)
                                : -1;
       float oyv, ozv;
-      bool tie = false;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq, tie);
-      if constexpr (LP == 2) {
-        // a pixel near an rgba8 tie lists its quad (the 2x2 pixels of one
-        // output chroma sample) for the exact pass: one atomic per wave
-        // (a ballot's popcount), the quad leaders' slots by mbcnt
-        const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
-        const bool lead = quad_sum(tie ? 1.0f : 0.0f) > 0.0f && (lane & 3) == 0 && px < F.W && py < F.H;
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(lead);
-        if (m) {
-          unsigned base = 0;
-          if (lane == 0) base = atomicAdd(F.nt_count, (unsigned)__builtin_popcountll(m));
-          base = __builtin_amdgcn_readfirstlane(base);
-          const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          if (lead)
-            F.nt_list[base + below] = ((unsigned)g.f * (unsigned)F.ch + (unsigned)(py >> 1)) * (unsigned)F.cw + (unsigned)(px >> 1);
-        }
-      }
+          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
       if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
@@ -1197,8 +1171,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   X(0, 8, 0, 0)       \
   X(0, 7, 0, 1)       \
   X(0, 8, 0, 1)       \
-  X(0, 7, 0, 2)       \
-  X(0, 8, 0, 2)       \
   X(0, 4, 0, 1)       \
   X(0, 5, 0, 1)       \
   X(0, 6, 0, 1)       \
@@ -1215,8 +1187,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H2S_TILE_WP
   X(1, 8, 0, 0)       \
   X(1, 7, 0, 1)       \
   X(1, 8, 0, 1)       \
-  X(1, 7, 0, 2)       \
-  X(1, 8, 0, 2)       \
   X(1, 4, 0, 1)       \
   X(1, 5, 0, 1)       \
   X(1, 6, 0, 1)

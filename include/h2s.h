@@ -221,8 +221,6 @@ enum h2s_option {
 #define H2S_OPT_TEST_FAIL_AFTER_LAUNCH (H2S_OPT_PRIVATE_BASE + 1)
 /* peak statistics kernel form (A/B measurements): 0 = row chunks (default), 1 = 2 x 8 chunks */
 #define H2S_OPT_TEST_PEAK_FORM (H2S_OPT_PRIVATE_BASE + 2)
-/* the near-tie window of H2S_OPT_LP_EXACT 1, in units of 1e-9 (default 6000) */
-#define H2S_OPT_TEST_NT_WINDOW (H2S_OPT_PRIVATE_BASE + 3)
 #endif
 
 /* Kernel path h2s_process takes for a given frame pair (h2s_query_path). */

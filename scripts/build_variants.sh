@@ -28,10 +28,9 @@ for spec in "$@"; do
     fi
     /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $MMC $flags -c -o "$V/fast_$name.o" "$C/h2s_fast.hip" &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fastlp_$name.o" "$C/h2s_fast_lp.hip" &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fastlpx_$name.o" "$C/h2s_fast_lpx.hip" &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" "$V/fastlp_$name.o" "$V/fastlpx_$name.o" \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" "$V/fastlp_$name.o" \
       "$d345" "$d12" "$O/h2s_api.hip.o" "$O/h2s_kernels.hip.o" \
-      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o" "$V/fastlp_$name.o" "$V/fastlpx_$name.o" "$V/dbg12_$name.o" "$V/dbg345_$name.o"
+      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o" "$V/fastlp_$name.o" "$V/dbg12_$name.o" "$V/dbg345_$name.o"
   ) &
   pids+=($!)
 done

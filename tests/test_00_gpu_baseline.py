@@ -105,9 +105,8 @@ def _lp_exact_bound(params, got, want, W, H):
     assert d.max(initial=0) <= step, f'max diff {d.max()} > one step ({step}); {(d > step).sum()} samples beyond'
 
 
-@pytest.mark.parametrize('mode', [1, 2])   # 1: tile kernel + near-tie exact pass; 2: the generic kernel
 @pytest.mark.parametrize('kind', ['smooth', 'website'])
-def test_c3_lp_exact_full_size_within_one_step(kind, mode):
+def test_c3_lp_exact_full_size_within_one_step(kind):
     """C3 (4K BT.2390, libplacebo branch, 65^3) with H2S_OPT_LP_EXACT on a
     smooth synthetic frame and the reference's own website frame: max diff
     one output step."""
@@ -125,18 +124,16 @@ def test_c3_lp_exact_full_size_within_one_step(kind, mode):
     else:
         src = synth_frames(kind, 1, W, H, 10, device='cpu', seed=11)
     t = hdr2sdr.Tonemapper(0, params, lattice(65))
-    t.set_option(_abi.OPT_LP_EXACT, mode)
+    t.set_option(_abi.OPT_LP_EXACT, 1)
     got = t(src.to_torch('cuda')).to_numpy().buf.astype(np.int64)
     t.close()
     want = oracle.process(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, W, H).astype(np.int64)
     _lp_exact_bound(params, got, want, W, H)
 
 
-@pytest.mark.parametrize('mode', [1, 2])
-def test_c3_lp_exact_4k_sequence_within_one_step(mode):
+def test_c3_lp_exact_4k_sequence_within_one_step():
     """The 5-frame C3 peak_detect sequence above, with H2S_OPT_LP_EXACT: max
-    diff one output step on every frame (mode 1: the exact pass reads each
-    frame's own curve record)."""
+    diff one output step on every frame."""
     import json
     import os
     import numpy as np
@@ -151,7 +148,7 @@ def test_c3_lp_exact_4k_sequence_within_one_step(mode):
     W, H = 3840, 2160
     buf = sequence(W, H)[:5]
     t = hdr2sdr.Tonemapper(0, params, lattice(65))
-    t.set_option(_abi.OPT_LP_EXACT, mode)
+    t.set_option(_abi.OPT_LP_EXACT, 1)
     src = hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)
     dst = hdr2sdr.FrameBatch.empty_numpy(5, W, H, 10)
     t.process(src, dst)

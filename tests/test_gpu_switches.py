@@ -396,25 +396,20 @@ def test_rgb48_debug_stage4_matches_oracle(tm):
     assert (d < 1.5 / 65535).mean() > 0.95
 
 
-# H2S_OPT_LP_EXACT over the branch's cases without eq (eq after the quantiser
-# spreads a one-step difference): mode 1 (the tile kernel's near-tie
-# instances + k_process's exact pass over the listed quads; the cases it does
-# not cover take the generic kernel) and mode 2 (the generic kernel) against
-# the oracle, every sample within one output step, on whole tiles and on
+# H2S_OPT_LP_EXACT (the branch on the generic kernel: the oracle's operation
+# order, glibc's powf / expf, the IPT form in double) over the branch's cases
+# without eq (eq after the quantiser spreads a one-step difference) against
+# the oracle: every sample within one output step, on whole tiles and on
 # tiles + tail columns
-@pytest.mark.parametrize('mode', [1, 2])
 @pytest.mark.parametrize('W,H', [(128, 64), (200, 96)])
 @pytest.mark.parametrize('kind', ['smooth', 'uniform', 'ramp', 'edges'])
 @pytest.mark.parametrize('case', sorted(c for c in LP_CASES if LP_CASES[c].get('gamma', 1.0) == 1.0))
-def test_libplacebo_lp_exact_within_one_step(tm, case, kind, W, H, mode):
+def test_libplacebo_lp_exact_within_one_step(tm, case, kind, W, H):
     params = hdr2sdr.TonemapParams(**LP_CASES[case])
-    tm.set_option(_abi.OPT_LP_EXACT, mode)
+    tm.set_option(_abi.OPT_LP_EXACT, 1)
     try:
         got, want, wh = run_both(tm, params, kind, W, H)
-        if mode == 1 and W % 64 == 0:
-            # the near-tie instances serve BT.2390 / spline on the IPT form with the LUT on
-            nt = (params.tonemapper in ('bt.2390', 'spline') and params.lp_tone == 'ipt' and params.lut_enabled)
-            assert _path(tm, params, W, H) == (_abi.PATH_TILE if nt else _abi.PATH_GENERIC)
+        assert _path(tm, params, W, H) == _abi.PATH_GENERIC
     finally:
         tm.set_option(_abi.OPT_LP_EXACT, 0)
     op = oracle.params_from(params.to_c())
