@@ -152,6 +152,23 @@ def cpu_baseline(params, lattice, width, height, budget_s):
     return rec
 
 
+def workload_label(args, W, H, n, B):
+    """The line's workload string (roofline.traffic is keyed on it): BASELINE's
+    C2 for the default arguments; a profiling run of another chain names its
+    own config (C3: the libplacebo branch's BT.2390; otherwise the operator,
+    pipeline and peak detection)."""
+    c2 = (args.tonemapper == 'hable' and args.gamma == 2.2 and args.pipeline == 'auto' and not args.peak_detect
+          and args.transfer == 'smpte2084')
+    c3 = (args.tonemapper == 'bt.2390' and args.gamma == 1.0 and args.pipeline in ('auto', 'libplacebo')
+          and args.transfer == 'smpte2084')
+    tag = 'C2' if c2 else ('C3' if c3 else 'profiling run')
+    extra = '' if c2 else (f', pipeline {args.pipeline}, lp_tone {args.lp_tone}'
+                           + (', peak_detect=1' if args.peak_detect else ''))
+    return (f'{tag}: {W}x{H} {"HLG" if args.transfer != "smpte2084" else "PQ HDR10"} yuv420p{args.bits_in}le -> '
+            f'yuv420p{args.bits_out}le, {args.tonemapper} + {n}^3 tetrahedral LUT + eq gamma {args.gamma}, '
+            f'mode {args.mode}{extra}, {B} frames per launch')
+
+
 def pmc_traffic(workload):
     """HBM bytes per k_tile dispatch from the committed PMC passes
     (scripts/profile.sh -> prof_summary.py -> profiles/<round>/traffic.json),
@@ -461,9 +478,7 @@ def main():
         'dtype': 'f32',
         'data': 'synthetic',
         'config': {
-            'workload': (f'C2: {W}x{H} PQ HDR10 yuv420p{args.bits_in}le -> yuv420p{args.bits_out}le, '
-                         f'{args.tonemapper} + {n}^3 tetrahedral LUT + eq gamma {args.gamma}, mode {args.mode}, '
-                         f'{B} frames per launch'),
+            'workload': workload_label(args, W, H, n, B),
             'frames_per_rank_per_step': B,
             'width': W, 'height': H,
             'content': args.kind,

@@ -33,6 +33,7 @@ struct PeakModel {
   double npx;                         // pixels per frame
   int nblocks;                        // partial records per frame
   int pct;                            // percentile < 100: histograms present
+  int family;                         // the curve the records serve: 7 BT.2390, 8 spline, else libplacebo NORM
 };
 
 // the smoothing state carried from frame to frame and call to call
@@ -194,13 +195,15 @@ __host__ __device__ inline void curve_fast(const K& k, CurveConsts* cc) {
   cc->n_mob_scale = k.n_mob_scale;
 }
 
-// the complete per-frame record for a smoothed peak (units of 100 nits) and
-// average PQ level
+// the per-frame record for a smoothed peak (units of 100 nits) and average
+// PQ level: the constants of the launch's curve family (the others stay
+// zero; each family's double-precision setup is several pow calls, and the
+// records of a launch are made in one block on the critical path)
 __host__ __device__ inline void curve_for_peak(const PeakModel& m, double peak, double avg_pq, CurveConsts* cc) {
-  CurveConsts plain;
-  bt2390_consts(peak, m.t_white, m.t_black, m.knee_off, &plain);
-  spline_consts(peak, avg_pq, m.contrast, m.t_white, m.t_black, &plain);
-  lp_norm_consts(peak, m.tm_param, m.t_white, &plain);
+  CurveConsts plain{};
+  if (m.family == 7) bt2390_consts(peak, m.t_white, m.t_black, m.knee_off, &plain);
+  else if (m.family == 8) spline_consts(peak, avg_pq, m.contrast, m.t_white, m.t_black, &plain);
+  else lp_norm_consts(peak, m.tm_param, m.t_white, &plain);
   curve_fast(plain, cc);
 }
 

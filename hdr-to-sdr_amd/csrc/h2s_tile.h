@@ -57,9 +57,6 @@
 namespace h2s {
 
 typedef float f3 __attribute__((ext_vector_type(3)));
-#ifndef H2S_PQI_DIRECT
-#define H2S_PQI_DIRECT 1   // 0: PQ encodes below the table's first octave clamp to it (A/B)
-#endif
 #ifndef H2S_CELL_LAYOUT
 #define H2S_CELL_LAYOUT 0   // 1: the cell-major lattice A/B (h2s_fast.hip): the r stride from FastParams
 #endif
@@ -135,28 +132,26 @@ __device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log
 
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
 // (build_pqi_table): the segment is the float's exponent and top three
-// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); octaves
-// 2^-34 .. 2^14 (clamped at the top: the IPT form caps its input at 1e6 npl).
-// Eight segments per octave, not four: the LMS encode error the decode
-// amplifies (x ~11-45 through the EOTF's slope) drops from ~1e-6 to the
-// float32 floor, and the libplacebo branch's rgba8 download flips 7x less
-// often (scripts/c3_table_flips.py).  Below 2^-34 (3e-7 nits: black) the
-// direct form, ((c1 + c2 y^m1) / (1 + c3 y^m1))^m2 on v_log / v_exp, in a
-// divergent branch only the lanes there take (black frames' areas: whole waves)
+// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); clamped to the
+// table's octaves 2^-64 .. 2^14 (the IPT form caps its input at 1e6 npl;
+// below 2^-64, 1e-15 nits, the first segment's value is within 3e-7 of PQ(0)).
+// The near-black octaves matter: an LMS row of a dark pixel on synthetic
+// content reaches 1e-13, and clamping at 2^-40 (PQ 1.4e-5 instead of down to
+// 7.3e-7) put 0.5 % errors on stage-2 values of 1e-5.  y <= 0 (black, or an
+// LMS row of a saturated colour) is PQ(0) = c1^m2 exactly, as the oracle's
+// max(y, 0).  Eight segments per octave, not four (round 5): the LMS encode
+// error the decode amplifies (x ~11-45 through the EOTF's slope) drops from
+// ~1e-6 to the float32 floor (scripts/c3_table_flips.py: the rgba8 download
+// flips this table alone causes drop 7x); the 10 KB table puts the libplacebo
+// instances above 32 KB of LDS, i.e. at 4 blocks per CU
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
-  // y <= 0 (an LMS row of a saturated colour can go negative) encodes as 0,
-  // as the oracle's max(y, 0): the bit pattern clamps to +0, the direct form
-  const unsigned b = (unsigned)max((int)__builtin_bit_cast(unsigned, y), 0);
-  const int sr = (int)(b >> 20) - ((127 + PQI_OCT0) << 3);
-  const int sg = min(max(sr, 0), PQI_NSEG - 1);
+  const int yi = (int)__builtin_bit_cast(unsigned, y);
+  const unsigned b = (unsigned)max(yi, 0);
+  const int sg = min(max((int)(b >> 20) - ((127 + PQI_OCT0) << 3), 0), PQI_NSEG - 1);
   const float t = __builtin_bit_cast(float, (b & 0xFFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
-  float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
-  if (H2S_PQI_DIRECT && sr < 0) {
-    const float ym = fexp2(flog2(__builtin_bit_cast(float, b)) * PQ_M1);   // y = 0: log2 -> -inf, ym = 0
-    v = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
-  }
-  return v;
+  const float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
+  return yi > 0 ? v : 7.309559e-07f;
 }
 
 // S1 transfer to linear (units of npl), specialised
@@ -684,10 +679,6 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   }
   if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
-  if (F.eq_ident) {   // launch-uniform: the identity table is not staged
-    if constexpr (EQM) return (uint16_t)__builtin_bit_cast(unsigned, o.x + 8388608.0f);
-    return (uint16_t)(int)o.x;
-  }
   if constexpr (EQM) {
     // o.x = the luma quantiser input less 0.5 (the lattice records carry no
     // +0.5): adding 2^23 rounds it to the nearest integer in the mantissa's
@@ -714,9 +705,15 @@ constexpr int CBW = 32, CBH = 16;  // chroma tile
 // 2-way: 34 % -> 20 % of LDS-active cycles in bank conflicts, time unchanged;
 // profiles/r04/ablations/lds_stride.txt).  68 on the libplacebo instances,
 // whose PQ-encode table and native-depth eq table leave no room: +1.1 KB there
-// drops them from 5 blocks per CU to 4 (C3 +9 %)
+// drops them from 5 blocks per CU to 4 (C3 +9 %).  Round 5: their 8-segment
+// PQ-encode table puts them at 4 blocks per CU anyway; 72 measured the same
+// as 68 there (0.939 / 0.936 ms, profiles/r05/lp_variants.log), 68 kept for
+// the LDS (the 12-bit output's 8 KB eq table)
+#ifndef H2S_YST_LP
+#define H2S_YST_LP 68
+#endif
 template <int LP>
-constexpr int row_stride() { return LP ? 68 : H2S_YST; }
+constexpr int row_stride() { return LP ? H2S_YST_LP : H2S_YST; }
 // buffer-op aux bits: non-temporal (streamed frame bytes).  Frame loads that
 // bypass the L1 (sc1 nt, sc0 sc1 nt) or use workgroup scope (sc0 nt) time the
 // same within 1 %: the streamed bytes do not evict the lattice lines the
@@ -981,8 +978,11 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 #ifndef H2S_TILE_WPE
 #define H2S_TILE_WPE 5
 #endif
+// the libplacebo instances: the same 5 waves per SIMD for the register
+// budget (96 VGPRs, 2-6 spilled); 4 (106 VGPRs, no spills) measured 8 %
+// slower with the PQ-encode table's branch-free form (profiles/r05/lp_variants.log)
 #ifndef H2S_TILE_WPE_LP
-#define H2S_TILE_WPE_LP H2S_TILE_WPE   // the libplacebo instances (A/B)
+#define H2S_TILE_WPE_LP H2S_TILE_WPE
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TILE_WPE_LP : H2S_TILE_WPE))) void k_tile(
     const FastParams F) {
@@ -1019,8 +1019,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   }
   // codes at the output depth: shift, or bit replication (h2s_expand;
   // rep_rs = 8 - shift, or 31 for a plain shift: the 8-bit code >> 31 = 0)
-  if (!F.eq_ident && t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
-  for (int i = t + 256; !F.eq_ident && i < F.eq_n; i += 256) {  // native 10/12-bit tables
+  if (t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
+  for (int i = t + 256; i < F.eq_n; i += 256) {  // native 10/12-bit tables
     const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
     eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
   }

@@ -15,7 +15,7 @@ from hdr2sdr import _abi  # noqa: E402
 from hdr2sdr.synth import synth_frames  # noqa: E402
 from ipt_cond import ipt_channel_scale  # noqa: E402
 
-EPS_IPT = 1e-4
+EPS_IPT = 2e-5
 LAT = hdr2sdr.generate_lattice(65)
 W, H = 128, 64
 tm = hdr2sdr.Tonemapper(0)
