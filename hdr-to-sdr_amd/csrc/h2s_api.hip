@@ -59,7 +59,6 @@ struct h2s_ctx {
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
   uint16_t* d_eq = nullptr;
-  bool eq_ident = false;   // the resolved eq table maps every code to itself
   float4* d_pq = nullptr;  // PQ EOTF cubic segments (fast path)
   float4* d_hlg = nullptr; // HLG inverse-OETF cubic segments (fast path, CPU chain)
   float4* d_pqi = nullptr; // PQ inverse EOTF cubic segments (fast path, lp_tone IPT)
@@ -815,8 +814,6 @@ int h2s_set_params(h2s_ctx* c, const h2s_params* p) {
   }
   hipError_t e = table_copy(c, c->d_eq, eq.data(), eq.size() * sizeof(uint16_t));
   if (e != hipSuccess) return hip_fail(c, e, "eq table upload");
-  c->eq_ident = true;
-  for (int i = 0; i <= k.qmax && i < (int)eq.size(); i++) c->eq_ident = c->eq_ident && eq[i] == i;
   {
     std::vector<float4> pq;
     // (x 10000/npl for either input transfer: the libplacebo branch's IPT form
@@ -942,7 +939,6 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->lut_bytes = 12 * n * n * n;
   F->eq_lut = c->d_eq;
   F->eq_n = k.qmax + 1;
-  F->eq_ident = c->eq_ident && k.shift_out == 0 ? 1 : 0;
   F->c_bias = 128.0f * k.qscale + 0.5f;
   F->shift_out = k.shift_out;
   F->rep_rs = k.expand_rep && k.shift_out ? 8 - k.shift_out : 31;

@@ -195,8 +195,6 @@ struct FastParams : CurveConsts {
   // S6..S8
   const uint16_t* eq_lut;
   int eq_n;
-  int eq_ident;                    // the eq table is the identity at the output depth (the libplacebo
-                                   // instances then neither stage nor read it)
   float c_bias;
   int shift_out, out8;
   int rep_rs;                      // S8: 8 - shift_out (bit replication) or 31 (shift)
@@ -224,9 +222,9 @@ constexpr int TBW = 64, TBH = 32;   // k_tile: luma tile of one block
 constexpr int PQ_SEG = 128;          // segments per unit of E
 constexpr int PQ_NSEG = 240;         // table covers E in [0, 1.875)
 constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
-constexpr int PQI_OCT0 = -48;        // PQ encode table: first octave 2^-48 (x 10000 nits)
+constexpr int PQI_OCT0 = -64;        // PQ encode table: first octave 2^-64 (x 10000 nits)
 constexpr int PQI_PER_OCT = 8;       // segments per octave (exponent + top 3 mantissa bits)
-constexpr int PQI_NSEG = 49 * PQI_PER_OCT;   // octaves 2^-48 .. 2^1 (above: the direct form)
+constexpr int PQI_NSEG = 78 * PQI_PER_OCT;   // octaves 2^-64 .. 2^14
 
 struct YuvLutConsts {
   float s, k709[3], kcb[3], kcr[3];

@@ -96,7 +96,7 @@ hipError_t launch_fast(const FastParams& F0, int trc, int tm, int desat, int lp,
   // (5 blocks per CU, the LDS bound; 4 and 3, forced by padding this
   // allocation, measured +4 % and +42 % on the bench content:
   // profiles/r03/ablations/blocks_per_cu.log)
-  const size_t lds = lp && F.eq_ident ? 0 : ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
+  const size_t lds = ((size_t)F.eq_n * sizeof(uint16_t) + 15) & ~(size_t)15;
   if (tm == 7 || tm == 8 || lp) desat = 0;
 #define H2S_DISPATCH(D) \
   return lp ? launch_tile<D, 1>(F, trc, tm, desat, grid, lds, s) : launch_tile<D, 0>(F, trc, tm, desat, grid, lds, s)

@@ -132,30 +132,25 @@ __device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log
 
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
 // (build_pqi_table): the segment is the float's exponent and top three
-// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); octaves 2^-48
-// .. 2^1.  y <= 0 (black, or an LMS row of a saturated colour) is PQ(0) =
-// c1^m2 exactly, as the oracle's max(y, 0); below 2^-48 (3e-11 nits) the
-// first segment's value is within 2.2e-6 of the curve; above 2^1 (20,000
-// nits: codes past the EOTF's range only, never on real content) the direct
-// form ((c1 + c2 y^m1) / (1 + c3 y^m1))^m2 on v_log / v_exp, in a divergent
-// branch only those lanes take.  Eight segments per octave, not four (round
-// 5): the LMS encode error the decode amplifies (x ~11-45 through the EOTF's
-// slope) drops from ~1e-6 to the float32 floor (scripts/c3_table_flips.py:
-// the rgba8 download flips this table alone causes drop 7x).  The range is
-// what keeps the libplacebo instances at 5 blocks per CU: 6.1 KB of table,
-// 32,744 B of LDS with the identity eq table unstaged (eq_ident)
+// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); clamped to the
+// table's octaves 2^-64 .. 2^14 (the IPT form caps its input at 1e6 npl;
+// below 2^-64, 1e-15 nits, the first segment's value is within 3e-7 of PQ(0)).
+// The near-black octaves matter: an LMS row of a dark pixel on synthetic
+// content reaches 1e-13, and clamping at 2^-40 (PQ 1.4e-5 instead of down to
+// 7.3e-7) put 0.5 % errors on stage-2 values of 1e-5.  y <= 0 (black, or an
+// LMS row of a saturated colour) is PQ(0) = c1^m2 exactly, as the oracle's
+// max(y, 0).  Eight segments per octave, not four (round 5): the LMS encode
+// error the decode amplifies (x ~11-45 through the EOTF's slope) drops from
+// ~1e-6 to the float32 floor (scripts/c3_table_flips.py: the rgba8 download
+// flips this table alone causes drop 7x); the 10 KB table puts the libplacebo
+// instances above 32 KB of LDS, i.e. at 4 blocks per CU
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
   const int yi = (int)__builtin_bit_cast(unsigned, y);
   const unsigned b = (unsigned)max(yi, 0);
-  const int sr = (int)(b >> 20) - ((127 + PQI_OCT0) << 3);
-  const int sg = min(max(sr, 0), PQI_NSEG - 1);
+  const int sg = min(max((int)(b >> 20) - ((127 + PQI_OCT0) << 3), 0), PQI_NSEG - 1);
   const float t = __builtin_bit_cast(float, (b & 0xFFFFFu) | 0x3F800000u) - 1.0f;
   const float4 c = tab[sg];
-  float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
-  if (sr >= PQI_NSEG) {
-    const float ym = fexp2(flog2(y) * PQ_M1);
-    v = fexp2(flog2((PQ_C1 + PQ_C2 * ym) * frcp(1.0f + PQ_C3 * ym)) * PQ_M2);
-  }
+  const float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
   return yi > 0 ? v : 7.309559e-07f;
 }
 
@@ -684,9 +679,6 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   }
   if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
-  if constexpr (LP) {
-    if (F.eq_ident) return (uint16_t)(int)o.x;   // launch-uniform: the identity table is not staged
-  }
   if constexpr (EQM) {
     // o.x = the luma quantiser input less 0.5 (the lattice records carry no
     // +0.5): adding 2^23 rounds it to the nearest integer in the mantissa's
@@ -713,8 +705,10 @@ constexpr int CBW = 32, CBH = 16;  // chroma tile
 // 2-way: 34 % -> 20 % of LDS-active cycles in bank conflicts, time unchanged;
 // profiles/r04/ablations/lds_stride.txt).  68 on the libplacebo instances,
 // whose PQ-encode table and native-depth eq table leave no room: +1.1 KB there
-// drops them from 5 blocks per CU to 4 (C3 +9 %; round 5 at 4 blocks per CU:
-// 72 and 68 measured the same, 0.939 / 0.936 ms, profiles/r05/lp_variants.log)
+// drops them from 5 blocks per CU to 4 (C3 +9 %).  Round 5: their 8-segment
+// PQ-encode table puts them at 4 blocks per CU anyway; 72 measured the same
+// as 68 there (0.939 / 0.936 ms, profiles/r05/lp_variants.log), 68 kept for
+// the LDS (the 12-bit output's 8 KB eq table)
 #ifndef H2S_YST_LP
 #define H2S_YST_LP 68
 #endif
@@ -984,8 +978,9 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 #ifndef H2S_TILE_WPE
 #define H2S_TILE_WPE 5
 #endif
-// the libplacebo instances: the same 5 waves per SIMD (96 VGPRs); 4 (106
-// VGPRs, no spills) measured 6-8 % slower (profiles/r05/lp_variants.log)
+// the libplacebo instances: the same 5 waves per SIMD for the register
+// budget (96 VGPRs, 2-6 spilled); 4 (106 VGPRs, no spills) measured 8 %
+// slower with the PQ-encode table's branch-free form (profiles/r05/lp_variants.log)
 #ifndef H2S_TILE_WPE_LP
 #define H2S_TILE_WPE_LP H2S_TILE_WPE
 #endif
@@ -1024,9 +1019,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   }
   // codes at the output depth: shift, or bit replication (h2s_expand;
   // rep_rs = 8 - shift, or 31 for a plain shift: the 8-bit code >> 31 = 0)
-  const bool stage_eq = !(LP && F.eq_ident);   // block-uniform
-  if (stage_eq && t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
-  for (int i = t + 256; stage_eq && i < F.eq_n; i += 256) {  // native 10/12-bit tables
+  if (t < F.eq_n) eq_lds[t] = (uint16_t)((eq0 << F.shift_out) | (eq0 >> F.rep_rs));
+  for (int i = t + 256; i < F.eq_n; i += 256) {  // native 10/12-bit tables
     const unsigned v = __builtin_amdgcn_raw_buffer_load_b16(req, 2 * i, 0, 0);
     eq_lds[i] = (uint16_t)((v << F.shift_out) | (v >> F.rep_rs));
   }
