@@ -514,19 +514,27 @@ def main():
         # k_tile's instruction mix from the same PMC passes (per pixel)
         rec['roofline']['instructions_per_px'] = {k: tr[k] for k in ('valu_per_px', 'trans_per_px', 'cvt_per_px',
                                                                       'lds_per_px', 'vmem_rd_per_px') if k in tr}
-        # the unit that actually binds, from the same
-        # PMC passes: VALU wave-instructions per CU-cycle (1.0 = the four
-        # SIMDs' issue peak), texture-data busy share; 'frac' stays the HBM
-        # fraction north_star's roofline asks for
-        for k in ('valu_issue_frac', 'valu_active_frac', 'td_busy_frac'):
+        # the unit that binds, from the same PMC passes
+        # (scripts/prof_summary.py unit_shares): VALU issue against the
+        # gfx950 rate (2 cycles per wave64 full-rate op per SIMD-32, 4 per
+        # transcendental), the texture data / address units' busy shares;
+        # 'frac' stays the HBM fraction north_star's roofline asks for
+        for k in ('valu_insts_per_cu_cycle', 'valu_issue_frac', 'valu_active_frac', 'td_busy_frac',
+                  'td_tc_stall_frac', 'ta_busy_frac'):
             if k in tr:
                 rec['roofline'][k] = tr[k]
-        if tr.get('valu_issue_frac', 0.0) > rec['roofline']['frac']:
-            rec['roofline']['bound'] = 'valu-issue'
-            rec['roofline']['bound_note'] = ('VALU issue %.2f of peak and texture-data unit %.2f busy (PMC) against '
-                                             'HBM %.2f: the kernel is issue-bound, not bandwidth-bound'
-                                             % (tr['valu_issue_frac'], tr.get('td_busy_frac', float('nan')),
-                                                rec['roofline']['frac']))
+        units = {'hbm': rec['roofline']['frac'], 'valu-issue': tr.get('valu_issue_frac', 0.0),
+                 'vmem-td': tr.get('td_busy_frac', 0.0)}
+        top = max(units, key=units.get)
+        if top != 'hbm':
+            rec['roofline']['bound'] = top
+            rec['roofline']['bound_note'] = (
+                'busiest unit by PMC: texture data (L1 -> VGPR) %.2f busy, %.2f of it waiting for the L1; '
+                'VALU issue %.2f of the gfx950 rate (%.2f wave-instructions per CU-cycle); HBM %.2f: the '
+                'lattice gathers and the frame I/O share the vector-memory path (DESIGN.md 4.1)'
+                % (tr.get('td_busy_frac', float('nan')), tr.get('td_tc_stall_frac', float('nan')),
+                   tr.get('valu_issue_frac', float('nan')), tr.get('valu_insts_per_cu_cycle', float('nan')),
+                   rec['roofline']['frac']))
     rec['config']['output_checksum'] = checksum
     if world == 1 and args.cpu_seconds > 0:
         rec['cpu_baseline'] = cpu_baseline(params, lattice_host, W, H, args.cpu_seconds)

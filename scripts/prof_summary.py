@@ -11,6 +11,63 @@ import os
 import sys
 from collections import defaultdict
 
+
+def unit_shares(m):
+    """What binds the kernel, from per-dispatch counter
+    means m.  GRBM_GUI_ACTIVE is summed over the 8 XCDs (32 CUs each).
+    - valu_insts_per_cu_cycle: SQ_INSTS_VALU / (cycles x 256), the figure
+      VERDICT r04 defined;
+    - valu_issue_frac: the same against the CU's VALU rate on gfx950 -- four
+      SIMD-32 units, a wave64 full-rate op 2 cycles, a transcendental 4
+      (MI355X_MICROARCH.md, constants table: v_fma 2 cyc; issue cost of one
+      wave alone v_exp 8 vs v_fma 4) -- i.e. (VALU + TRANS) / (cycles x 512).
+      1.0 is the ceiling; the C3 instance measures 1.15 VALU wave-instructions
+      per CU-cycle, so one per cycle is not;
+    - valu_active_frac: SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)
+      per SIMD-cycle -- counts waves waiting on their VALU, can pass 1;
+    - td_busy_frac / td_tc_stall_frac / ta_busy_frac: the texture data unit
+      (L1 -> VGPR return, one per CU) busy, and the share of it waiting for
+      the L1; the texture address unit."""
+    out = {}
+    if 'GRBM_GUI_ACTIVE' not in m:
+        return out
+    cyc = m['GRBM_GUI_ACTIVE'] / 8.0
+    out['cycles_per_dispatch'] = round(cyc)
+    if 'SQ_INSTS_VALU' in m:
+        out['valu_insts_per_cu_cycle'] = round(m['SQ_INSTS_VALU'] / (cyc * 256), 4)
+        out['valu_issue_frac'] = round((m['SQ_INSTS_VALU'] + m.get('SQ_INSTS_VALU_TRANS_F32', 0.0))
+                                       / (cyc * 512), 4)
+    if 'SQ_ACTIVE_INST_VALU' in m:
+        out['valu_active_frac'] = round(4 * m['SQ_ACTIVE_INST_VALU'] / (cyc * 1024), 4)
+    for key, ctr in (('td_busy_frac', 'TD_TD_BUSY_sum'), ('td_tc_stall_frac', 'TD_TC_STALL_sum'),
+                     ('ta_busy_frac', 'TA_TA_BUSY_sum')):
+        if ctr in m:
+            out[key] = round(m[ctr] / (cyc * 256), 4)
+    return out
+
+
+def from_summary(d):
+    """Re-derive the unit shares of an existing traffic.json from the counter
+    means its summary.txt lists (for runs whose raw CSVs were not kept)."""
+    m = {}
+    for line in open(os.path.join(d, 'summary.txt')):
+        parts = line.split()
+        if len(parts) == 3 and parts[2].startswith('(n=') and parts[0][:1].isupper():
+            m[parts[0]] = float(parts[1])
+    path = os.path.join(d, 'traffic.json')
+    rec = json.load(open(path))
+    for k in ('valu_issue_frac', 'valu_active_frac', 'td_busy_frac', 'cycles_per_dispatch'):
+        rec.pop(k, None)
+    rec.update(unit_shares(m))
+    with open(path, 'w') as f:
+        json.dump(rec, f, indent=1)
+    print('traffic.json:', json.dumps(rec))
+
+
+if len(sys.argv) > 2 and sys.argv[1] == '--from-summary':
+    from_summary(sys.argv[2])
+    sys.exit(0)
+
 d = sys.argv[1]
 # the C2 instance k_tile<PQ, Hable, RGB desat, CPU chain, DBG 0>
 KERNEL = os.environ.get('H2S_PROF_KERNEL', 'k_tile<0, 5, 2, 0, 0>')   # (H2S_PROF_KERNEL: another instance)
@@ -64,20 +121,7 @@ if 'FETCH_SIZE' in vals and 'WRITE_SIZE' in vals:
                          ('vmem_rd_per_px', 'SQ_INSTS_VMEM_RD')):
             if ctr in vals:
                 rec[key] = round(sum(vals[ctr]) / len(vals[ctr]) * 64 / px, 2)
-    # what binds the kernel: VALU wave-instructions
-    # issued per CU-cycle (one per cycle is the 4 SIMDs' peak for wave64 full-
-    # rate ops), the texture-data unit's busy share, per the cycles of the
-    # dispatch (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 32 CUs each)
-    if 'GRBM_GUI_ACTIVE' in vals:
-        cyc = sum(vals['GRBM_GUI_ACTIVE']) / len(vals['GRBM_GUI_ACTIVE']) / 8.0
-        rec['cycles_per_dispatch'] = round(cyc)
-        if 'SQ_INSTS_VALU' in vals:
-            rec['valu_issue_frac'] = round(sum(vals['SQ_INSTS_VALU']) / len(vals['SQ_INSTS_VALU']) / (cyc * 256), 4)
-        if 'SQ_ACTIVE_INST_VALU' in vals:
-            rec['valu_active_frac'] = round(4 * sum(vals['SQ_ACTIVE_INST_VALU']) / len(vals['SQ_ACTIVE_INST_VALU'])
-                                            / (cyc * 1024), 4)
-        if 'TD_TD_BUSY_sum' in vals:
-            rec['td_busy_frac'] = round(sum(vals['TD_TD_BUSY_sum']) / len(vals['TD_TD_BUSY_sum']) / (cyc * 256), 4)
+    rec.update(unit_shares({k: sum(v) / len(v) for k, v in vals.items()}))
     with open(os.path.join(d, 'traffic.json'), 'w') as f:
         json.dump(rec, f, indent=1)
     print('traffic.json:', json.dumps(rec))
