@@ -55,6 +55,7 @@ struct h2s_ctx {
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   bool fast_enabled = true;
   bool lp_exact = false;  // H2S_OPT_LP_EXACT
+  int peak_blocks = h2s::PEAK_BLOCKS;   // H2S_OPT_TEST_PEAK_BLOCKS (private A/B hook)
   int peak_form = 0;      // H2S_OPT_TEST_PEAK_FORM (private A/B hook)
   bool serial_host = false;  // H2S_HOST_SERIAL=1: one H2D, kernel, D2H per call (no chunk pipeline)
   int tiles_per_block = 8;  // k_tile: tiles one block walks (H2S_TILES_PER_BLOCK overrides, 1..64)
@@ -78,6 +79,14 @@ struct h2s_ctx {
   h2s::PeakState* d_pk = nullptr;         // [0] the smoothing state; [1] a preview's saved copy of it
   hipEvent_t peak_ev = nullptr;           // after the last launch that used the buffers above
   bool peak_pending = false;
+  // pipelined schedule (run_dynamic_peak_chunked; private A/B hook
+  // H2S_OPT_TEST_PEAK_CHUNK, off: measured slower): frames per
+  // chunk (0 = one statistics launch, then one conversion launch, all on the
+  // caller's stream), the statistics stream and a second conversion stream,
+  // events: start | end | per-chunk statistics
+  int peak_chunk = 0;
+  hipStream_t pk_s[2] = {};
+  std::vector<hipEvent_t> pk_ev;
   std::string err;
   bool fail_after_launch = false;  // H2S_OPT_TEST_FAIL_AFTER_LAUNCH (private test hook, one call)
   bool timing = false;
@@ -328,9 +337,9 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
     k->enc_a = (float)a;
     k->enc_b = (float)(lb / (1.0 - lb));
   }
-  h2s::bt2390_consts(peak, k->t_white, k->t_black, k->knee_off, k);
+  h2s::bt2390_consts(peak, k->t_white, k->t_black, k->knee_off, k, h2s::pq_refs(k->t_white, k->t_black));
   k->sp_contrast = isnan(p->tm_param) ? 0.5f : (float)p->tm_param;
-  h2s::spline_consts(peak, 0.0, (double)k->sp_contrast, k->t_white, k->t_black, k);
+  h2s::spline_consts(peak, 0.0, (double)k->sp_contrast, k->t_white, k->t_black, k, h2s::pq_refs(k->t_white, k->t_black));
   k->npl_1e4 = (float)(p->npl / 10000.0);
   k->e4_npl = (float)(10000.0 / k->t_white);
   k->ipt_npl = p->npl / 10000.0, k->ipt_os = 10000.0 / k->t_white, k->ipt_tw = k->t_white / 10000.0;
@@ -673,6 +682,9 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_chr) hipFree(c->d_chr);
   if (c->peak_ev) hipEventDestroy(c->peak_ev);
+  for (hipEvent_t ev : c->pk_ev) hipEventDestroy(ev);
+  for (hipStream_t ps : c->pk_s)
+    if (ps) hipStreamDestroy(ps);
   if (c->chr_ev) hipEventDestroy(c->chr_ev);
   for (hipEvent_t ev : c->pend) hipEventDestroy(ev);
   for (hipEvent_t ev : c->ev_free) hipEventDestroy(ev);
@@ -1182,9 +1194,10 @@ static h2s::PeakModel peak_model(const h2s_ctx* c, const KParams& k) {
   m.percentile = k.pd_percentile, m.min_peak = k.pd_min;
   m.iir_a = k.pd_smoothing > 0.0 ? 1.0 - exp(-1.0 / k.pd_smoothing) : 1.0;
   m.npx = (double)k.W * k.H;
-  m.nblocks = h2s::PEAK_BLOCKS;
+  m.nblocks = c->peak_blocks;
   m.pct = k.pd_percentile < 100.0 ? 1 : 0;
   m.family = k.tonemap;
+  m.pq = h2s::pq_refs(k.t_white, k.t_black);
   return m;
 }
 
@@ -1248,11 +1261,11 @@ static int peak_done(h2s_ctx* c, hipStream_t s) {
 // histograms and the counter are zero between launches (cleared at
 // allocation, left zero by the kernels)
 static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s, h2s::PeakState* st,
-                       h2s::CurveConsts* out) {
+                       h2s::CurveConsts* out, int f0 = 0) {
   const h2s::PeakModel m = peak_model(c, k);
   if (nframes > c->stats_nf) {
     const size_t nf = (size_t)nframes;
-    const size_t part = nf * h2s::PEAK_BLOCKS * sizeof(float2), zero = (nf * h2s::PEAK_BINS + 1) * sizeof(unsigned);
+    const size_t part = nf * h2s::PEAK_BLOCKS_MAX * sizeof(float2), zero = (nf * h2s::PEAK_BINS + 1) * sizeof(unsigned);
     if (c->d_stats) hipFree(c->d_stats);
     c->d_stats = nullptr;
     c->stats_nf = 0;
@@ -1264,14 +1277,15 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
     if (e != hipSuccess) return hip_fail(c, e, "peak statistics clear");
     c->stats_nf = nframes;
   }
-  if (int rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)nframes * sizeof(double2), "peak statistics"))
+  if (int rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)(f0 + nframes) * sizeof(double2),
+                         "peak statistics"))
     return rc;
   const size_t nf = (size_t)c->stats_nf;
   float2* d_part = static_cast<float2*>(c->d_stats);
   h2s::PeakTail T;
   T.M = m;
-  T.fstat = c->d_fstat;
-  T.hist = reinterpret_cast<unsigned*>(d_part + nf * h2s::PEAK_BLOCKS);
+  T.fstat = c->d_fstat + f0;
+  T.hist = reinterpret_cast<unsigned*>(d_part + nf * h2s::PEAK_BLOCKS_MAX);
   T.done = T.hist + nf * h2s::PEAK_BINS;
   T.st = st;
   T.out = out;
@@ -1279,6 +1293,72 @@ static int frame_stats(h2s_ctx* c, const KParams& k, int nframes, hipStream_t s,
   T.form = c->peak_form;
   hipError_t e = h2s::launch_peak_stats(k, d_part, T, s);
   return e == hipSuccess ? 0 : hip_fail(c, e, "peak statistics");
+}
+
+// k restricted to frames [f0, f0 + n)
+static KParams frame_range(const KParams& k, int f0, int n) {
+  KParams kf = k;
+  for (int p = 0; p < 3; p++) {
+    kf.in[p] += (long long)f0 * kf.in_fp[p];
+    kf.out[p] += (long long)f0 * kf.out_fp[p];
+  }
+  kf.nframes = n;
+  kf.total = (long long)n * kf.ch * kf.ngx;
+  return kf;
+}
+
+static int peak_streams(h2s_ctx* c, int nev) {
+  for (hipStream_t& ps : c->pk_s)
+    if (!ps) {
+      hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+      if (e != hipSuccess) {
+        ps = nullptr;
+        return hip_fail(c, e, "peak stream");
+      }
+    }
+  while ((int)c->pk_ev.size() < nev) {
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(c, e, "peak event");
+    c->pk_ev.push_back(ev);
+  }
+  return 0;
+}
+
+// The pipelined schedule (tile kernel, whole tiles): the statistics of chunk
+// j + 1 run on their own stream while chunk j converts, and consecutive
+// chunks convert on alternating streams, so that neither a chunk boundary
+// nor the statistics leave the chip idle.  The state still advances frame by
+// frame in order (the statistics stream is serial), exactly as one launch.
+static int run_dynamic_peak_chunked(h2s_ctx* c, const KParams& k, bool vec, bool out8, int nframes, hipStream_t s) {
+  const int C = c->peak_chunk, nch = (nframes + C - 1) / C;
+  int rc;
+  // every allocation before the first launch (hipFree of a grown buffer
+  // would wait for the device)
+  if ((rc = peak_streams(c, nch + 2)) ||
+      (rc = ensure_dev(c, (void**)&c->d_fstat, &c->fstat_cap, (size_t)nframes * sizeof(double2), "peak statistics")))
+    return rc;
+  hipStream_t ss = c->pk_s[0], st[2] = {s, c->pk_s[1]};
+  hipEvent_t ev_start = c->pk_ev[0], ev_end = c->pk_ev[1];
+  hipError_t e = hipEventRecord(ev_start, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(ss, ev_start, 0);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st[1], ev_start, 0);
+  if (e != hipSuccess) return hip_fail(c, e, "peak schedule");
+  for (int j = 0; j < nch; j++) {
+    const int f0 = j * C, n = std::min(C, nframes - f0);
+    const KParams kj = frame_range(k, f0, n);
+    if ((rc = frame_stats(c, kj, n, ss, c->d_pk, c->d_curve + f0, f0))) return rc;
+    hipEvent_t ev = c->pk_ev[2 + j];
+    if ((e = hipEventRecord(ev, ss)) != hipSuccess || (e = hipStreamWaitEvent(st[j & 1], ev, 0)) != hipSuccess)
+      return hip_fail(c, e, "peak schedule");
+    if ((e = launch_chain(c, kj, true, vec, out8, n, st[j & 1], c->d_curve + f0, false)) != hipSuccess)
+      return hip_fail(c, e, "kernel launch");
+  }
+  // s joins the statistics stream (the state) and the second conversion stream
+  if ((e = hipEventRecord(ev_end, st[1])) != hipSuccess || (e = hipStreamWaitEvent(s, ev_end, 0)) != hipSuccess ||
+      (e = hipStreamWaitEvent(s, c->pk_ev[2 + nch - 1], 0)) != hipSuccess)
+    return hip_fail(c, e, "peak schedule");
+  return peak_done(c, s);
 }
 
 // statistics, then the frames in order, each with the BT.2390 / spline
@@ -1291,6 +1371,8 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
   if ((rc = ensure_peak_state(c)) || (rc = peak_order(c, s))) return rc;
   if ((rc = ensure_dev(c, (void**)&c->d_curve, &c->curve_cap, (size_t)nframes * sizeof(h2s::CurveConsts), "curve records")))
     return rc;
+  if (fast && (k.W & (h2s::TBW - 1)) == 0 && c->peak_chunk > 0 && nframes > c->peak_chunk)
+    return run_dynamic_peak_chunked(c, k, vec, out8, nframes, s);
   if ((rc = frame_stats(c, k, nframes, s, c->d_pk, c->d_curve))) return rc;
   hipError_t e;
   if (fast) {
@@ -1299,13 +1381,7 @@ static int run_dynamic_peak(h2s_ctx* c, const KParams& k, bool fast, bool vec, b
   }
   if (!fast || (k.W & (h2s::TBW - 1)) != 0) {
     for (int f = 0; f < nframes; f++) {
-      KParams kf = k;
-      for (int p = 0; p < 3; p++) {
-        kf.in[p] += f * kf.in_fp[p];
-        kf.out[p] += f * kf.out_fp[p];
-      }
-      kf.nframes = 1;
-      kf.total = (long long)kf.ch * kf.ngx;
+      KParams kf = frame_range(k, f, 1);
       kf.cv = c->d_curve + f;
       e = fast ? launch_tail(kf, 1, vec, out8, s, h2s::TBW) : launch_chain(c, kf, false, vec, out8, 1, s);
       if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
@@ -1669,6 +1745,14 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
       return 0;
     case H2S_OPT_TEST_PEAK_FORM:
       c->peak_form = (int)value;
+      return 0;
+    case H2S_OPT_TEST_PEAK_BLOCKS:
+      if (value < 1 || value > h2s::PEAK_BLOCKS_MAX) return fail(c, H2S_E_INVALID_ARG, "peak blocks must be in [1, 256]");
+      c->peak_blocks = (int)value;
+      return 0;
+    case H2S_OPT_TEST_PEAK_CHUNK:
+      if (value < 0 || value > 4096) return fail(c, H2S_E_INVALID_ARG, "peak chunk must be in [0, 4096]");
+      c->peak_chunk = (int)value;
       return 0;
     default:
       return fail(c, H2S_E_INVALID_ARG, "unknown option");

@@ -351,8 +351,8 @@ hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float
 // pixel (libplacebo peak detection, src/utils.py:448; PARITY UNPINNED: no
 // libplacebo here, model in DESIGN.md).  PQ sources: PQ(max(EOTF(E))) ==
 // clamp(max(E), 0, 1) exactly, so no transcendental is needed.  Chroma is
-// taken nearest (the statistic is an estimate).  grid = (PEAK_BLOCKS, frames);
-// partial[f * PEAK_BLOCKS + b] = (max, sum) over the rows b, b + PEAK_BLOCKS, ...
+// taken nearest (the statistic is an estimate).  grid = (M.nblocks, frames);
+// partial[f * M.nblocks + b] = (max, sum) over block b's rows / chunks
 // one pixel's PQ-domain max(R,G,B) from its integer codes (nearest chroma)
 template <int TRC>
 __device__ __forceinline__ float peak_px(const KParams& P, unsigned yc, unsigned uc, unsigned vc) {
@@ -425,8 +425,8 @@ __device__ void peak_frame_fold(const float2* partial, unsigned* hist, const Pea
   __shared__ double s_mx, s_sum;
   __shared__ unsigned long long s_scan[256];
   __shared__ int s_bin;
-  __shared__ float2 s_part[PEAK_BLOCKS];
-  static_assert(PEAK_BLOCKS <= 256, "one partial record per thread");
+  __shared__ float2 s_part[PEAK_BLOCKS_MAX];
+  static_assert(PEAK_BLOCKS_MAX <= 256, "one partial record per thread");
   if (t < M.nblocks) s_part[t] = partial[(size_t)f * M.nblocks + t];   // all loads in flight at once
   __syncthreads();
   if (t == 0) {
@@ -557,6 +557,9 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
 // rounding is monotonic).  Fewer loads and VALU per pixel, yet measured 165 us
 // against 104 us for 16 4K frames (round 5, profiles/r05/peak_ab): the default
 // stays the row form
+#ifndef H2S_PEAK_INFLIGHT
+#define H2S_PEAK_INFLIGHT 4
+#endif
 template <int TRC, bool HIST, bool ROW2 = false>
 __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, const PeakTail T) {
   __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
@@ -632,15 +635,17 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
     }
     sm += rs;
   };
+  // H2S_PEAK_INFLIGHT chunks' loads issued before the first is folded (the
+  // kernel is latency-bound: one block-wave of 64 blocks per frame)
   int i = blockIdx.x * 256 + threadIdx.x;
-  for (; i + stride < nch; i += 2 * stride) {
-    Chunk c0, c1;
-    load(i, c0);
-    load(i + stride, c1);
-    fold(c0);
-    fold(c1);
+  for (; i + (H2S_PEAK_INFLIGHT - 1) * stride < nch; i += H2S_PEAK_INFLIGHT * stride) {
+    Chunk c[H2S_PEAK_INFLIGHT];
+#pragma unroll
+    for (int k = 0; k < H2S_PEAK_INFLIGHT; k++) load(i + k * stride, c[k]);
+#pragma unroll
+    for (int k = 0; k < H2S_PEAK_INFLIGHT; k++) fold(c[k]);
   }
-  if (i < nch) {
+  for (; i < nch; i += stride) {
     Chunk c;
     load(i, c);
     fold(c);
@@ -655,7 +660,7 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
 // two launches
 hipError_t launch_peak_stats(const KParams& P, float2* partial, const PeakTail& T, hipStream_t s) {
   if (P.nframes <= 0) return hipSuccess;
-  const dim3 grid(PEAK_BLOCKS, P.nframes);
+  const dim3 grid(T.M.nblocks, P.nframes);
   auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
   const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
                    al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&

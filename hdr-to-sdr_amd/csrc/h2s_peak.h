@@ -20,8 +20,17 @@
 
 namespace h2s {
 
-constexpr int PEAK_BLOCKS = 64;  // partial (max, sum) records per frame (k_peak_stats*)
+constexpr int PEAK_BLOCKS = 64;       // partial (max, sum) records per frame (k_peak_stats*), default
+constexpr int PEAK_BLOCKS_MAX = 256;  // ... at most (H2S_OPT_TEST_PEAK_BLOCKS A/B; one per finish thread)
 constexpr int PEAK_BINS = 1024;  // percentile histogram bins over PQ [0, 1]
+
+// the PQ levels of the SDR target that every curve set-up needs: PQ(0), PQ of
+// the target white and black (nits / 10000), pq_refs below.  Host-made once
+// per launch for the device's per-frame records, so that k_peak_finish's
+// serial tail spends its double-precision powers on the frame's peak only
+struct PqRefs {
+  double smin, white, black;
+};
 
 // the launch-constant inputs of a frame's curve (resolved h2s_params)
 struct PeakModel {
@@ -34,6 +43,7 @@ struct PeakModel {
   int nblocks;                        // partial records per frame
   int pct;                            // percentile < 100: histograms present
   int family;                         // the curve the records serve: 7 BT.2390, 8 spline, else libplacebo NORM
+  PqRefs pq;                          // pq_refs(t_white, t_black), host-made
 };
 
 // the smoothing state carried from frame to frame and call to call
@@ -73,6 +83,10 @@ __host__ __device__ inline double hd_pq_eotf(double e) {
   return pow(num / (c2 - c3 * xp), 1.0 / m1);
 }
 
+__host__ __device__ inline PqRefs pq_refs(double t_white, double t_black) {
+  return PqRefs{hd_pq_encode(0.0), hd_pq_encode(t_white / 10000.0), hd_pq_encode(t_black / 10000.0)};
+}
+
 __host__ __device__ inline float hd_hable(float in) {
   const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
   return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
@@ -101,10 +115,11 @@ __host__ __device__ inline void lp_norm_consts(double peak, double tm_param, dou
 // knee ks = (1 + offset) maxLum - offset, black-point adaptation exponent
 // bp = min(1 / minLum, 4) and gain 1 / (1 + minLum / maxLum (1 - maxLum)^bp)
 template <class K>
-__host__ __device__ inline void bt2390_consts(double peak, double t_white, double t_black, double knee_off, K* k) {
-  const double smin = hd_pq_encode(0.0), smax = hd_pq_encode(peak * 100.0 / 10000.0);
-  const double ml = (hd_pq_encode(t_white / 10000.0) - smin) / (smax - smin);
-  const double mn = t_black > 0.0 ? (hd_pq_encode(t_black / 10000.0) - smin) / (smax - smin) : 0.0;
+__host__ __device__ inline void bt2390_consts(double peak, double t_white, double t_black, double knee_off, K* k,
+                                              const PqRefs& r) {
+  const double smin = r.smin, smax = hd_pq_encode(peak * 100.0 / 10000.0);
+  const double ml = (r.white - smin) / (smax - smin);
+  const double mn = t_black > 0.0 ? (r.black - smin) / (smax - smin) : 0.0;
   const double ks = (1.0 + knee_off) * ml - knee_off;
   const double bp = mn > 0.0 ? fmin(1.0 / mn, 4.0) : 4.0;
   k->b_srcmin = (float)smin;
@@ -127,7 +142,7 @@ __host__ __device__ inline void bt2390_consts(double peak, double t_white, doubl
 // 0.2).  avg_pq: the frame's average PQ level (peak detection), 0 = unknown.
 template <class K>
 __host__ __device__ inline void spline_consts(double peak, double avg_pq, double contrast, double t_white,
-                                              double t_black, K* k) {
+                                              double t_black, K* k, const PqRefs& r) {
   const double kad = 0.4, kmin = 0.1, kmax = 0.8, kdef = 0.4, st = 1.5, so = 0.2;
   auto mix = [](double a, double b, double t) { return a + (b - a) * t; };
   auto smooth = [](double e0, double e1, double x) {
@@ -135,8 +150,9 @@ __host__ __device__ inline void spline_consts(double peak, double avg_pq, double
     t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
     return t * t * (3.0 - 2.0 * t);
   };
-  const double smin = hd_pq_encode(0.0), smax = hd_pq_encode(peak * 100.0 / 10000.0);
-  const double dmin = hd_pq_encode(t_black / 10000.0), dmax = hd_pq_encode(t_white / 10000.0);
+  (void)t_white, (void)t_black;
+  const double smin = r.smin, smax = hd_pq_encode(peak * 100.0 / 10000.0);
+  const double dmin = r.black, dmax = r.white;
   double sk = avg_pq > 0.0 ? avg_pq : mix(smin, smax, kdef);
   sk = fmin(fmax(sk, mix(smin, smax, kmin)), mix(smin, smax, kmax));
   const double target = (sk - smin) / (smax - smin);
@@ -201,8 +217,8 @@ __host__ __device__ inline void curve_fast(const K& k, CurveConsts* cc) {
 // records of a launch are made in one block on the critical path)
 __host__ __device__ inline void curve_for_peak(const PeakModel& m, double peak, double avg_pq, CurveConsts* cc) {
   CurveConsts plain{};
-  if (m.family == 7) bt2390_consts(peak, m.t_white, m.t_black, m.knee_off, &plain);
-  else if (m.family == 8) spline_consts(peak, avg_pq, m.contrast, m.t_white, m.t_black, &plain);
+  if (m.family == 7) bt2390_consts(peak, m.t_white, m.t_black, m.knee_off, &plain, m.pq);
+  else if (m.family == 8) spline_consts(peak, avg_pq, m.contrast, m.t_white, m.t_black, &plain, m.pq);
   else lp_norm_consts(peak, m.tm_param, m.t_white, &plain);
   curve_fast(plain, cc);
 }

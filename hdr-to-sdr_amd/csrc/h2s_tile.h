@@ -441,7 +441,7 @@ struct StepK {
 // debug planes (DBG > 0, frame 0), else -1.
 template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
-                                             const float4* pqi_lds, const uint16_t* eq_lds,
+                                             const float4* pqi_lds, const uint16_t* eq_lds, const float2* lut8_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
                                              long long di, float& oyv, float& ozv, float qoff, float ydq) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
@@ -511,18 +511,21 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
     o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
   } else {
-    float sr, sg, sb;
+    // lattice cell origins (cr, cg, cb) and fractions (dr, dg, db) per channel
+    float cr, cg, cb, dr, dg, db;
     if (LP) {
       // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the
-      // range=tv and rounding / dither offsets, h2s_lp_range / _dither), then
-      // lut3d's 8-bit coordinate (q / 255) (N-1) in its own operation order:
-      // q = 255 lands on N-1 exactly (fract 0: the corners past the lattice
-      // edge get weight 0 and read in-bounds records or the buffer's zero fill)
-      auto q8 = [&](float x) -> float {
+      // range=tv and rounding / dither offsets, h2s_lp_range / _dither; all
+      // >= 0, so the conversion's truncation is the floor), then lut3d's
+      // 8-bit coordinate (q / 255) (N-1) in its own operation order, read as
+      // (cell, fraction) from the block's 256-entry table (lut8_lds, made in
+      // the prologue by the same float operations): q = 255 lands on N-1
+      // exactly (fraction 0: the corners past the lattice edge get weight 0
+      // and read in-bounds records or the buffer's zero fill)
+      auto q8 = [&](float x) -> unsigned {
         const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
+        return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
       };
-      const float qr = q8(r), qg = q8(gg), qb = q8(bl);
       if (DBG == 3) {
         auto ev = [&](float x) {
           const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
@@ -530,8 +533,18 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
         };
         dput(ev(r), ev(gg), ev(bl));
       }
-      sr = qr * F.inv255 * F.nm1, sg = qg * F.inv255 * F.nm1, sb = qb * F.inv255 * F.nm1;
+#if H2S_LP_LUT8TAB
+      const float2 tr = lut8_lds[q8(r)], tg = lut8_lds[q8(gg)], tb = lut8_lds[q8(bl)];
+      cr = tr.x, dr = tr.y, cg = tg.x, dg = tg.y, cb = tb.x, db = tb.y;
+#else   // A/B: the per-pixel statement the table replaces
+      float sr = (float)q8(r) * F.inv255 * F.nm1, sg = (float)q8(gg) * F.inv255 * F.nm1,
+            sb = (float)q8(bl) * F.inv255 * F.nm1;
+      asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
+      dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
+      cr = sr - dr, cg = sg - dg, cb = sb - db;
+#endif
     } else {
+      float sr, sg, sb;
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, K.x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
 #if H2S_EXPCLAMP
@@ -548,16 +561,17 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
       sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
 #endif
+      // s is a product when N-1 is not a power of two (N-1 times the clamped
+      // power): without this barrier the compiler contracts the cell origin
+      // s - fract(s) below into fma(N-1, x, -fract(s)), which carries the
+      // product's rounding error, so the origin is no longer an integer and a
+      // byte offset truncates to a misaligned record (N = 177: 45 of 3072
+      // samples of a uniform frame)
+      asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
+      dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
+      cr = sr - dr, cg = sg - dg, cb = sb - db;
     }
-    // s is a product when N-1 is not a power of two (N-1 times the clamped
-    // power; 8-bit code / 255 x (N-1) on the libplacebo branch): without this
-    // barrier the compiler contracts the cell origin s - fract(s) below into
-    // fma(N-1, x, -fract(s)), which carries the product's rounding error, so the
-    // origin is no longer an integer and a byte offset truncates to a
-    // misaligned record (N = 177: 45 of 3072 samples of a uniform frame)
-    asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
-    const float dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-    const int base = (int)fmaf(sb - db, K.stride_b, fmaf(sg - dg, K.stride_g, (sr - dr) * (H2S_CELL_LAYOUT ? K.stride_r : 12.0f)));
+    const int base = (int)fmaf(cb, K.stride_b, fmaf(cg, K.stride_g, cr * (H2S_CELL_LAYOUT ? K.stride_r : 12.0f)));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
     // fractions: the 4 low mantissa bits of each fraction carry its axis a
     // (bits 3:2 and 1:0 both = a; r 0, g 1, b 2; a change of <= 2^-19
@@ -669,7 +683,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
       o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
     }
-    if (DBG == 3 && !LP) dput(sr * F.inv_nm1, sg * F.inv_nm1, sb * F.inv_nm1);
+    if (DBG == 3 && !LP) dput((cr + dr) * F.inv_nm1, (cg + dg) * F.inv_nm1, (cb + db) * F.inv_nm1);   // = s exactly
     if (DBG == 4 && !LP) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
       const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
                    q3 = F.dbg_lut[(base + F.c111) / 12];
@@ -981,6 +995,11 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 // the libplacebo instances: the same 5 waves per SIMD for the register
 // budget (96 VGPRs, 2-6 spilled); 4 (106 VGPRs, no spills) measured 8 %
 // slower with the PQ-encode table's branch-free form (profiles/r05/lp_variants.log)
+// the libplacebo instances' lut3d 8-bit coordinates from the block's 256-entry
+// (cell, fraction) table (0: per pixel, as before round 5's A/B)
+#ifndef H2S_LP_LUT8TAB
+#define H2S_LP_LUT8TAB 1
+#endif
 #ifndef H2S_TILE_WPE_LP
 #define H2S_TILE_WPE_LP H2S_TILE_WPE
 #endif
@@ -992,6 +1011,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
   __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
+  __shared__ float2 lut8_lds[LP ? 256 : 1];    // lut3d 8-bit coordinate per rgba code: (cell, fraction)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
@@ -1032,6 +1052,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
   if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
+  if (LP) {   // (q / 255) (N-1) as px_chain's former per-pixel statement, and its fraction
+    float sq = (float)t * F.inv255 * F.nm1;
+    asm("" : "+v"(sq));   // no contraction of sq - dq into fma(.., F.nm1, -dq): see px_chain
+    const float dq = __builtin_amdgcn_fractf(sq);
+    lut8_lds[t] = make_float2(sq - dq, dq);
+  }
   __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
     const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
@@ -1100,7 +1126,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
+          F, cv, pq_lds, pqi_lds, eq_lds, lut8_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
       if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it

@@ -42,6 +42,8 @@ OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL, OPT_LP_EXACT = 1, 2, 3, 4
 # private test hook (include/h2s.h H2S_PRIVATE_TEST_HOOKS: not part of the ABI)
 OPT_TEST_FAIL_AFTER_LAUNCH = 0x7f000000 + 1
 OPT_TEST_PEAK_FORM = 0x7f000000 + 2
+OPT_TEST_PEAK_CHUNK = 0x7f000000 + 3
+OPT_TEST_PEAK_BLOCKS = 0x7f000000 + 4
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
 ABI_VERSION = 3
 ABI_MINOR = 3   # include/h2s.h H2S_ABI_MINOR (the loaded library may be newer, not older)

@@ -221,6 +221,11 @@ enum h2s_option {
 #define H2S_OPT_TEST_FAIL_AFTER_LAUNCH (H2S_OPT_PRIVATE_BASE + 1)
 /* peak statistics kernel form (A/B measurements): 0 = row chunks (default), 1 = 2 x 8 chunks */
 #define H2S_OPT_TEST_PEAK_FORM (H2S_OPT_PRIVATE_BASE + 2)
+/* dynamic peak on the tile kernel: frames per pipelined chunk (0 = statistics for
+ * the whole batch, then one conversion launch) */
+#define H2S_OPT_TEST_PEAK_CHUNK (H2S_OPT_PRIVATE_BASE + 3)
+/* peak statistics: blocks (partial records) per frame, 1..256 (default 64) */
+#define H2S_OPT_TEST_PEAK_BLOCKS (H2S_OPT_PRIVATE_BASE + 4)
 #endif
 
 /* Kernel path h2s_process takes for a given frame pair (h2s_query_path). */

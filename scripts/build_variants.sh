@@ -26,11 +26,17 @@ for spec in "$@"; do
       /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$d12" "$C/h2s_fast_dbg12.hip" &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$d345" "$C/h2s_fast_dbg345.hip" || exit 1
     fi
+    # KERN=1: h2s_kernels.hip (generic kernel, peak statistics) gets the flags too
+    kern="$O/h2s_kernels.hip.o"
+    if [ "${KERN:-0}" = 1 ]; then
+      kern="$V/kern_$name.o"
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS -ffp-contract=off $flags -c -o "$kern" "$C/h2s_kernels.hip" || exit 1
+    fi
     /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $MMC $flags -c -o "$V/fast_$name.o" "$C/h2s_fast.hip" &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $flags -c -o "$V/fastlp_$name.o" "$C/h2s_fast_lp.hip" &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libh2s_$name.so" "$V/fast_$name.o" "$V/fastlp_$name.o" \
-      "$d345" "$d12" "$O/h2s_api.hip.o" "$O/h2s_kernels.hip.o" \
-      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o" "$V/fastlp_$name.o" "$V/dbg12_$name.o" "$V/dbg345_$name.o"
+      "$d345" "$d12" "$O/h2s_api.hip.o" "$kern" \
+      "$O/h2s_preview.hip.o" "$O/h2s_cube.cpp.o" && rm -f "$V/fast_$name.o" "$V/fastlp_$name.o" "$V/dbg12_$name.o" "$V/dbg345_$name.o" "$V/kern_$name.o"
   ) &
   pids+=($!)
 done

@@ -135,6 +135,44 @@ def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline, mo
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('pipeline', ['cpu', 'libplacebo'])
+@pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])   # pipelined schedule; tail width keeps the serial one
+def test_gpu_dynamic_peak_chunked_schedule_is_identical(W, H, pipeline):
+    """The pipelined dynamic-peak schedule (statistics of chunk j + 1 on
+    their own stream beside chunk j's conversion; chunks converted on two
+    streams, H2S_OPT_TEST_PEAK_CHUNK frames each, ragged last chunk included)
+    gives the unchunked schedule's output and state bit for bit, across calls,
+    and matches the oracle's sequential flow."""
+    import torch
+    from hdr2sdr import _abi
+    from test_gpu_parity import assert_close_int, lattice
+    seq = sequence(W, H)
+    buf = np.concatenate([seq, seq[::-1]])           # 12 frames, three scene cuts
+    n = buf.shape[0]
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0, pipeline=pipeline)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    src = hdr2sdr.FrameBatch(torch.from_numpy(np.ascontiguousarray(buf)).cuda(), W, H, 10)
+    dst = hdr2sdr.FrameBatch.empty_torch(n, W, H, 10, 'cuda')
+    runs = {}
+    for chunk in (0, 1, 4, 5, 12):
+        tm.set_option(_abi.OPT_TEST_PEAK_CHUNK, chunk)
+        tm.reset_peak()
+        outs = []
+        for _ in range(2):                           # the state carries into the second call
+            tm.process(src, dst)
+            torch.cuda.synchronize()
+            outs.append(dst.buf.cpu().numpy().copy())
+        runs[chunk] = (outs, tm.peak_state())
+    tm.close()
+    for chunk in (1, 4, 5, 12):
+        assert runs[chunk][1] == runs[0][1], chunk
+        for a, b in zip(runs[chunk][0], runs[0][0]):
+            assert np.array_equal(a, b), chunk
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    assert_close_int(params, runs[4][0][0].astype(np.int64), want.astype(np.int64), W, H)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('kw', [dict(chroma_filter='bicubic'), dict(gamma=1.3, dither='ordered', lp_dither='ordered'),
                                 dict(lp_range='limited', bits_out=8)])
 def test_gpu_dynamic_peak_with_switches_matches_oracle(kw):
