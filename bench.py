@@ -378,7 +378,7 @@ def main():
                  7680, 4320, 4, 65),
                 # the reference's other GPU-only operator (libplacebo spline), C3's shape
                 ('C3_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
-                # C3 with libplacebo's peak_detect=1 (src/utils.py:448): stats launch, host IIR, one tile launch
+                # C3 with libplacebo's peak_detect=1 (src/utils.py:448): statistics + finish (device IIR, curve records), one tile launch
                 ('C3_dyn', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=True, maxcll=4000.0),
                  3840, 2160, 16, 65)):
             p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
@@ -386,14 +386,14 @@ def main():
             src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)
             dst_ = hdr2sdr.FrameBatch.empty_torch(nf, w_, h_, p_.bits_out, dev)
             st_ = torch.cuda.current_stream(dev)
-            for _ in range(2):
+            for _ in range(3):
                 t_.process(src_, dst_, st_)
             torch.cuda.synchronize(dev)
             t_.set_timing(True)
-            for _ in range(5):
+            for _ in range(20):
                 t_.process(src_, dst_, st_)
             torch.cuda.synchronize(dev)
-            kms_ = t_.kernel_ms(5)
+            kms_ = t_.kernel_ms(20)
             b_ = 1.5 * (1 if p_.bits_in == 8 else 2) + 1.5 * (1 if p_.bits_out == 8 else 2)
             other[tag] = {'size': f'{w_}x{h_}', 'frames': nf, 'tonemapper': kw['tonemapper'], 'lut': lut_n,
                           'bits': f"{p_.bits_in}->{p_.bits_out}", 'kernel_ms': round(kms_, 4),

@@ -60,6 +60,9 @@ typedef float f3 __attribute__((ext_vector_type(3)));
 #ifndef H2S_CELL_LAYOUT
 #define H2S_CELL_LAYOUT 0   // 1: the cell-major lattice A/B (h2s_fast.hip): the r stride from FastParams
 #endif
+#ifndef H2S_LP_LUT8TAB
+#define H2S_LP_LUT8TAB 1   // libplacebo lut3d 8-bit coordinates from the block's (cell, fraction) table; 0: per pixel (A/B)
+#endif
 #ifndef H2S_LP_BLEND_FUSED
 #define H2S_LP_BLEND_FUSED 0   // 1: the libplacebo blend contracted into FMAs (pre-round-5 code, A/B)
 #endif
@@ -536,9 +539,12 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
 #if H2S_LP_LUT8TAB
       const float2 tr = lut8_lds[q8(r)], tg = lut8_lds[q8(gg)], tb = lut8_lds[q8(bl)];
       cr = tr.x, dr = tr.y, cg = tg.x, dg = tg.y, cb = tb.x, db = tb.y;
-#else   // A/B: the per-pixel statement the table replaces
-      float sr = (float)q8(r) * F.inv255 * F.nm1, sg = (float)q8(gg) * F.inv255 * F.nm1,
-            sb = (float)q8(bl) * F.inv255 * F.nm1;
+#else   // A/B: the per-pixel statement the table replaces (round 5 before the table)
+      auto q8f = [&](float x) -> float {
+        const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
+        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
+      };
+      float sr = q8f(r) * F.inv255 * F.nm1, sg = q8f(gg) * F.inv255 * F.nm1, sb = q8f(bl) * F.inv255 * F.nm1;
       asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
       dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
       cr = sr - dr, cg = sg - dg, cb = sb - db;
@@ -995,11 +1001,6 @@ template <int TRC, int TM, int DESAT, int LP, int DBG = 0>
 // the libplacebo instances: the same 5 waves per SIMD for the register
 // budget (96 VGPRs, 2-6 spilled); 4 (106 VGPRs, no spills) measured 8 %
 // slower with the PQ-encode table's branch-free form (profiles/r05/lp_variants.log)
-// the libplacebo instances' lut3d 8-bit coordinates from the block's 256-entry
-// (cell, fraction) table (0: per pixel, as before round 5's A/B)
-#ifndef H2S_LP_LUT8TAB
-#define H2S_LP_LUT8TAB 1
-#endif
 #ifndef H2S_TILE_WPE_LP
 #define H2S_TILE_WPE_LP H2S_TILE_WPE
 #endif

@@ -233,6 +233,17 @@ def test_lut_sizes(tm, lut_n):
     assert tm.query_path(src, dst) == (_abi.PATH_TILE if lut_n <= 177 else _abi.PATH_GENERIC)
 
 
+@pytest.mark.parametrize('lut_n', [2, 17, 33, 129, 177])
+def test_lut_sizes_libplacebo(tm, lut_n):
+    """lut3d's 8-bit path on the libplacebo branch at other lattice sizes:
+    k_tile<..., LP=1> takes each channel's (cell, fraction) from its 256-entry
+    LDS table of (q / 255) (N-1) (h2s_tile.h lut8_lds), N - 1 a power of two
+    or not; the rgba code 255 lands on the last node."""
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', pipeline='libplacebo')
+    got, want, src_wh = run_both(tm, params, 'uniform', 64, 32, lut_n=lut_n)
+    assert_close_int(params, got, want, *src_wh)
+
+
 # 1e-3 relative on the float path (north_star), per stage, on the kernel that
 # produces the output: k_tile's own debug instance (H2S_OPT_FAST_PATH 1, the
 # tile path) and the generic kernel (FAST_PATH 0).  The gate itself (what is
