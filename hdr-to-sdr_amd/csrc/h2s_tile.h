@@ -60,6 +60,9 @@ typedef float f3 __attribute__((ext_vector_type(3)));
 #ifndef H2S_CELL_LAYOUT
 #define H2S_CELL_LAYOUT 0   // 1: the cell-major lattice A/B (h2s_fast.hip): the r stride from FastParams
 #endif
+#ifndef H2S_LDS_BOX
+#define H2S_LDS_BOX 0   // 1: the LDS-staged lattice box on the CPU chain (A/B, px_chain)
+#endif
 #ifndef H2S_LP_LUT8TAB
 #define H2S_LP_LUT8TAB 1   // libplacebo lut3d 8-bit coordinates from the block's (cell, fraction) table; 0: per pixel (A/B)
 #endif
@@ -435,6 +438,8 @@ struct StepK {
   int c111;                       // the far corner's byte offset
   float nm1;                      // N - 1
   const int* offtab;              // LDS: byte offset of the +1 corner along r, g, b at bytes 0, 4, 8
+  float* box;                     // H2S_LDS_BOX: this wave's 4 x 4 x 4-node box (64 x 3 floats)
+  int boxofs;                     // ... byte offset of this lane's box node from the anchor cell's origin
 };
 
 // One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
@@ -672,10 +677,39 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
         return f3{L[i], L[i + 1], L[i + 2]};
       };
       o = blend(sl(b0), sl(b0 + m0), sl(b0 + n0), sl(b0 + F.c111));
-    } else
-    o = blend(__builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0), __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0),
-              __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0),
-              __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0));
+    } else {
+#if H2S_LDS_BOX
+      // A/B: the LDS-staged lattice box.  When every
+      // lane's cell lies within one cell of lane 0's, the wave loads the 4 x 4
+      // x 4 nodes around it with ONE gather (lane l: node l) into its 768-B
+      // LDS box and reads the four corners from there, instead of four
+      // gathers.  Same records, same blend: bit-identical
+      bool boxed = false;
+      if constexpr (TAG) {
+        auto rfl = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+        const float xr = cr - rfl(cr) + 1.0f, xg = cg - rfl(cg) + 1.0f, xb = cb - rfl(cb) + 1.0f;
+        const bool fit = xr == __builtin_amdgcn_fmed3f(xr, 0.0f, 2.0f) && xg == __builtin_amdgcn_fmed3f(xg, 0.0f, 2.0f) &&
+                         xb == __builtin_amdgcn_fmed3f(xb, 0.0f, 2.0f);
+        if (__builtin_amdgcn_ballot_w64(!fit) == 0 && __builtin_amdgcn_read_exec() == ~0ull) {
+          const int ba = __builtin_amdgcn_readfirstlane(base);
+          const f3 nd = __builtin_amdgcn_raw_buffer_load_b96(lut, ba + K.boxofs, 0, 0);   // out of range -> 0 (unused nodes)
+          const int l3 = 3 * (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+          K.box[l3] = nd.x, K.box[l3 + 1] = nd.y, K.box[l3 + 2] = nd.z;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          const int bi = 3 * (int)fmaf(xb, 16.0f, fmaf(xg, 4.0f, xr));      // corner 0, in floats
+          const int omb = 3 << (amax >> 1), ocnb = 63 - (3 << ((umin & 12u) >> 1));   // +1 node: 3 / 12 / 48 floats
+          auto rd = [&](int i) { return f3{K.box[i], K.box[i + 1], K.box[i + 2]}; };
+          o = blend(rd(bi), rd(bi + omb), rd(bi + ocnb), rd(bi + 63));
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // reads done before the next step's writes
+          boxed = true;
+        }
+      }
+      if (!boxed)
+#endif
+      o = blend(__builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0), __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0),
+                __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0),
+                __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0));
+    }
     if (LP) {
       // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
       // Y'CbCr at depth q in the generic kernel's operation order; o = (luma
@@ -1016,6 +1050,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
+  __shared__ float lbox[H2S_LDS_BOX && !LP ? 4 * 192 : 1];   // H2S_LDS_BOX: one 64-node box per wave
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -1090,7 +1125,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
   const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, in_vgpr(F.stride_r), og, ob, ocr, ocg, ocb, log2_nm1, x_max,
-                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab};
+                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab,
+                lbox + (H2S_LDS_BOX && !LP ? 192 * w : 0),
+                ((lane & 3) - 1) * 12 + (((lane >> 2) & 3) - 1) * og + ((lane >> 4) - 1) * ob};
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
