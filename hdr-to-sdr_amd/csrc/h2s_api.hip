@@ -1344,20 +1344,28 @@ static int run_dynamic_peak_chunked(h2s_ctx* c, const KParams& k, bool vec, bool
   if (e == hipSuccess) e = hipStreamWaitEvent(ss, ev_start, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(st[1], ev_start, 0);
   if (e != hipSuccess) return hip_fail(c, e, "peak schedule");
+  // an error exit still joins what was queued on the two internal streams
+  // into s (best effort), so the caller's stream (and queued_exit's launch
+  // event) covers all of it
+  auto fail_joined = [&](int code) {
+    if (hipEventRecord(ev_end, st[1]) == hipSuccess) (void)hipStreamWaitEvent(s, ev_end, 0);
+    if (hipEventRecord(ev_start, ss) == hipSuccess) (void)hipStreamWaitEvent(s, ev_start, 0);
+    return code;
+  };
   for (int j = 0; j < nch; j++) {
     const int f0 = j * C, n = std::min(C, nframes - f0);
     const KParams kj = frame_range(k, f0, n);
-    if ((rc = frame_stats(c, kj, n, ss, c->d_pk, c->d_curve + f0, f0))) return rc;
+    if ((rc = frame_stats(c, kj, n, ss, c->d_pk, c->d_curve + f0, f0))) return fail_joined(rc);
     hipEvent_t ev = c->pk_ev[2 + j];
     if ((e = hipEventRecord(ev, ss)) != hipSuccess || (e = hipStreamWaitEvent(st[j & 1], ev, 0)) != hipSuccess)
-      return hip_fail(c, e, "peak schedule");
+      return fail_joined(hip_fail(c, e, "peak schedule"));
     if ((e = launch_chain(c, kj, true, vec, out8, n, st[j & 1], c->d_curve + f0, false)) != hipSuccess)
-      return hip_fail(c, e, "kernel launch");
+      return fail_joined(hip_fail(c, e, "kernel launch"));
   }
   // s joins the statistics stream (the state) and the second conversion stream
   if ((e = hipEventRecord(ev_end, st[1])) != hipSuccess || (e = hipStreamWaitEvent(s, ev_end, 0)) != hipSuccess ||
       (e = hipStreamWaitEvent(s, c->pk_ev[2 + nch - 1], 0)) != hipSuccess)
-    return hip_fail(c, e, "peak schedule");
+    return fail_joined(hip_fail(c, e, "peak schedule"));
   return peak_done(c, s);
 }
 
