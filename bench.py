@@ -386,19 +386,31 @@ def main():
             src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)
             dst_ = hdr2sdr.FrameBatch.empty_torch(nf, w_, h_, p_.bits_out, dev)
             st_ = torch.cuda.current_stream(dev)
-            for _ in range(3):
-                t_.process(src_, dst_, st_)
-            torch.cuda.synchronize(dev)
-            t_.set_timing(True)
-            for _ in range(20):
-                t_.process(src_, dst_, st_)
-            torch.cuda.synchronize(dev)
-            kms_ = t_.kernel_ms(20)
+
+            def timed_(t_):
+                for _ in range(3):
+                    t_.process(src_, dst_, st_)
+                torch.cuda.synchronize(dev)
+                t_.set_timing(True)
+                for _ in range(20):
+                    t_.process(src_, dst_, st_)
+                torch.cuda.synchronize(dev)
+                return t_.kernel_ms(20)
+
+            kms_ = timed_(t_)
             b_ = 1.5 * (1 if p_.bits_in == 8 else 2) + 1.5 * (1 if p_.bits_out == 8 else 2)
             other[tag] = {'size': f'{w_}x{h_}', 'frames': nf, 'tonemapper': kw['tonemapper'], 'lut': lut_n,
                           'bits': f"{p_.bits_in}->{p_.bits_out}", 'kernel_ms': round(kms_, 4),
                           'mpx_s': round(nf * w_ * h_ / kms_ / 1e3, 1),
                           'hbm_frac': round(b_ * nf * w_ * h_ / (kms_ / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if p_.peak_detect:
+                # the detection's own cost: the same call without peak_detect
+                # (same static peak, so the tile kernel's curve work matches)
+                t0_ = hdr2sdr.Tonemapper(local, p_.with_(peak_detect=False), hdr2sdr.generate_lattice(lut_n))
+                sms_ = timed_(t0_)
+                t0_.close()
+                other[tag]['static_same_peak_ms'] = round(sms_, 4)
+                other[tag]['peak_detect_overhead_ms'] = round(kms_ - sms_, 4)
             if p_.resolved_pipeline() == 'libplacebo':
                 # the libplacebo stage is a restatement (no libplacebo in the image):
                 # GPU = oracle is tested, the oracle itself is not pinned to libplacebo;
