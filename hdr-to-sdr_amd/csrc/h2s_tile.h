@@ -63,6 +63,9 @@ typedef float f3 __attribute__((ext_vector_type(3)));
 #ifndef H2S_LDS_BOX
 #define H2S_LDS_BOX 0   // 1: the LDS-staged lattice box on the CPU chain (A/B, px_chain)
 #endif
+#ifndef H2S_PATCH_WALK
+#define H2S_PATCH_WALK 0   // 1: a block's 8 tiles as a 4 x 2 patch (A/B, tile_geo_patch)
+#endif
 #ifndef H2S_LP_LUT8TAB
 #define H2S_LP_LUT8TAB 1   // libplacebo lut3d 8-bit coordinates from the block's (cell, fraction) table; 0: per pixel (A/B)
 #endif
@@ -842,6 +845,20 @@ __device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) 
   return g;
 }
 
+// A/B (H2S_PATCH_WALK): a block's 8 tiles as a 4 x 2 patch (256 x 64
+// pixels) instead of a 1 x 8 row (512 x 32): tile t -> patch t / 8, tile t % 8
+// at (t % 4, t / 4 % 2) within it; patches in x, then y, then frame order.
+// Needs nbx % 4 == 0, nby % 2 == 0 and 8 tiles per block
+__device__ __forceinline__ TileGeo tile_geo_patch(const FastParams& F, unsigned tile) {
+  const unsigned st = tile >> 3, w = tile & 7u, sbx = F.nbx >> 2, sby = F.nby >> 1;
+  const unsigned sx = st % sbx, r = st / sbx;
+  const unsigned bx = 4 * sx + (w & 3u), by = 2 * (r % sby) + (w >> 2);
+  TileGeo g;
+  g.f = (int)(r / sby);
+  g.px0 = (int)bx * TBW, g.py0 = (int)by * TBH, g.cx0 = (int)bx * CBW, g.cy0 = (int)by * CBH;
+  return g;
+}
+
 // the tile after g in walk order (x, then y, then frame): block-uniform
 // scalar arithmetic, no division
 __device__ __forceinline__ void tile_next(const FastParams& F, TileGeo& g) {
@@ -1062,7 +1079,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const unsigned tend = tile + (unsigned)F.tpb < ntiles ? tile + (unsigned)F.tpb : ntiles;
 
   // ---- prologue: first tile + tables, all issued before any wait ----
+#if H2S_PATCH_WALK
+  const bool patch = (F.nbx & 3u) == 0 && (F.nby & 1u) == 0 && F.tpb == 8;   // block-uniform
+  TileGeo geo = patch ? tile_geo_patch(F, tile) : tile_geo(F, tile);
+#else
   TileGeo geo = tile_geo(F, tile);
+#endif
   const LaneOfs lofs = lane_ofs(F, t);
   TileRegs cur = tile_load(F, geo, t, lofs);
   const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
@@ -1199,6 +1221,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
+#if H2S_PATCH_WALK
+      if (patch)
+        geo = tile_geo_patch(F, tile + 1);
+      else
+#endif
       tile_next(F, geo);
       cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
