@@ -22,7 +22,9 @@ def unit_shares(m):
       (MI355X_MICROARCH.md, constants table: v_fma 2 cyc; issue cost of one
       wave alone v_exp 8 vs v_fma 4) -- i.e. (VALU + TRANS) / (cycles x 512).
       1.0 is the ceiling; the C3 instance measures 1.12-1.15 VALU wave-
-      instructions per CU-cycle, so one per cycle is not;
+      instructions per CU-cycle, so one per cycle is not.  Every other VALU
+      op counts at the full rate (a lower bound: compares, selects,
+      conversions, min/max and DPP measured ~1.65x, DESIGN.md §4.1);
     - valu_active_frac: SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)
       per SIMD-cycle -- counts waves waiting on their VALU, can pass 1;
     - td_busy_frac / td_tc_stall_frac / ta_busy_frac: the texture data unit
