@@ -128,6 +128,13 @@ def lib() -> ctypes.CDLL:
         L.oracle_tonemap_lin.restype = ctypes.c_int
         L.oracle_tonemap_lin.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_void_p]
+        L.oracle_set_lp_f32.restype = None
+        L.oracle_set_lp_f32.argtypes = [ctypes.c_int]
+        L.oracle_set_lp_bias.restype = None
+        L.oracle_set_lp_bias.argtypes = [ctypes.c_int]
+        L.oracle_lp_download.restype = ctypes.c_int
+        L.oracle_lp_download.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.POINTER(Frames), ctypes.c_void_p]
         L.oracle_preview_tail.restype = ctypes.c_int
         L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
@@ -202,6 +209,40 @@ def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray) -
     if rc:
         raise ValueError(f'oracle_tonemap_lin failed: {rc}')
     return out.reshape(shp)
+
+
+def lp_download(params: Params, lattice: np.ndarray, buf: np.ndarray, width: int, height: int) -> np.ndarray:
+    """libplacebo branch with the LUT: the exact (double) pre-rounding value x
+    of every rgba8 download channel of frame 0, [3, H, W] float64; the code is
+    floor(x).  The tie attribution of tests/lp_gate.py reads it."""
+    out = np.empty((3, height, width), dtype=np.float64)
+    din = _frames(np.ascontiguousarray(buf[:1]), width, height, params.bits_in)
+    lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
+    n = round(lat.shape[0] ** (1 / 3))
+    rc = lib().oracle_lp_download(ctypes.byref(params), lat.ctypes.data, n, ctypes.byref(din), out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_lp_download failed: {rc}')
+    return out
+
+
+class lp_form:
+    """Context manager: the libplacebo branch's stages 1-3 in the round-5
+    float32 form (f32=True) instead of exact arithmetic, and / or a bias of
+    `bias` codes on every rgba8 download code (the gate's mutation tests).
+    Process-wide; restores the defaults (exact, no bias) on exit."""
+
+    def __init__(self, f32: bool = False, bias: int = 0):
+        self.f32, self.bias = f32, bias
+
+    def __enter__(self):
+        lib().oracle_set_lp_f32(1 if self.f32 else 0)
+        lib().oracle_set_lp_bias(self.bias)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_lp_f32(0)
+        lib().oracle_set_lp_bias(0)
+        return False
 
 
 def preview_rgb24(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,

@@ -853,6 +853,230 @@ static inline float upsample(const ocfg *c, const h2s_frames *in, int plane, int
   return 0.75f * hpass(c, in, plane, frame, x, m, cw, ch) + 0.25f * hpass(c, in, plane, frame, x, m + 1, cw, ch);
 }
 
+/* ---- libplacebo branch, stages 1-3 as exact arithmetic (double) ----------
+ * The reference runs this branch's tone mapping in libplacebo's GLSL on a
+ * Vulkan GPU (src/utils.py:444-460): float32 shader arithmetic with the GPU's
+ * own transcendentals, never glibc's powf.  No float32 evaluation is "the"
+ * reference there, so the oracle states stages 1-3 of the branch as exact
+ * arithmetic -- double precision from the integer codes (chroma upsampled in
+ * double, the BT.2020-NCL matrix from kr / kb, the ST 2084 / ARIB B67
+ * constants, the curves of libplacebo's tone_mapping.c in double) -- down to
+ * the 8-bit rgba download's pre-rounding value x = v qs + qo + offset.  Any
+ * float32 implementation (libplacebo's, the tile kernel's, or this file's own
+ * round-5 float form, oracle_set_lp_f32) lands within its own error bound of
+ * x, and may round the download the other way only where x lies within that
+ * bound of an integer: tests/lp_gate.py attributes every such flip (VERDICT
+ * r05 item 1).  Stage 4 onwards (lut3d's 8-bit path on integer codes,
+ * Y'CbCr) keeps the float arithmetic of vf_lut3d / swscale. */
+static int g_lp_f32 = 0;   /* 1: the branch's stages 1-3 in the float32 form (chain_px) */
+static int g_lp_bias = 0;  /* test hook: added to every rgba8 download code (gate mutation tests) */
+
+typedef struct {
+  double r, g, b;
+} rgbd;
+
+/* normalised chroma / luma from the integer code, exactly */
+static inline double csamp_d(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
+  const int m = c->p->chroma_edge, sh = c->p->bits_in - 8;
+  const int v = rd(in, plane, frame, edge_m(x, cw, m), edge_m(y, ch, m)) & c->in_mask;
+  return ((double)v - (double)(128 << sh)) / (double)(224 << sh);
+}
+static inline double hpass_d(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int cy, int cw, int ch) {
+  int k = x >> 1;
+  if (!(x & 1)) return csamp_d(c, in, plane, frame, k, cy, cw, ch);
+  return 0.5 * (csamp_d(c, in, plane, frame, k, cy, cw, ch) + csamp_d(c, in, plane, frame, k + 1, cy, cw, ch));
+}
+static inline double upsample_d(const ocfg *c, const h2s_frames *in, int plane, int frame, int x, int y, int cw, int ch) {
+  int m = y >> 1;
+  if (!(y & 1)) return 0.25 * hpass_d(c, in, plane, frame, x, m - 1, cw, ch) + 0.75 * hpass_d(c, in, plane, frame, x, m, cw, ch);
+  return 0.75 * hpass_d(c, in, plane, frame, x, m, cw, ch) + 0.25 * hpass_d(c, in, plane, frame, x, m + 1, cw, ch);
+}
+
+/* ST 2084 EOTF (normalised), zimg's form (denominator floored at FLT_MIN) */
+static double pq_eotf_z(double e) {
+  if (!(e > 0.0)) return 0.0;
+  const double xp = pow(e, 1.0 / (double)PQ_M2);
+  const double num = xp - (double)PQ_C1 > 0.0 ? xp - (double)PQ_C1 : 0.0;
+  const double den = (double)PQ_C2 - (double)PQ_C3 * xp;
+  const double v = pow(num / (den > FLT_MIN ? den : FLT_MIN), 1.0 / (double)PQ_M1);
+  return v > FLT_MAX ? (double)INFINITY : v;   /* past the pole as the float form: +inf, not 1e238 */
+}
+
+/* ARIB STD-B67 inverse OETF with the specification's constants */
+static double hlg_inv_oetf_d(double x) {
+  const double a = 0.17883277, b = 0.28466892, cc = 0.55991073;
+  x = x > 0.0 ? x : 0.0;
+  return x <= 0.5 ? x * x / 3.0 : (exp((x - cc) / a) + b) / 12.0;
+}
+
+static double hable_d(double x) {
+  const double a = 0.15, b = 0.50, c = 0.10, d = 0.20, e = 0.02, f = 0.30;
+  return (x * (x * a + b * c) + d * e) / (x * (x * a + b) + d * f) - e / f;
+}
+
+/* lp_norm_curve in double */
+static double lp_norm_curve_d(const ocfg *c, double x) {
+  const double pk = c->n_peak;
+  x = x < 0.0 ? 0.0 : (x > pk ? pk : x);
+  switch (c->p->tonemap) {
+    case H2S_TM_REINHARD: {
+      const double ct = isnan(c->p->tm_param) ? 0.5 : c->p->tm_param;
+      const double off = (1.0 - ct) / ct, scale = (pk + off) / pk;
+      return scale * x / (x + off);
+    }
+    case H2S_TM_HABLE:
+      return hable_d(x) / hable_d(pk);
+    default: {
+      const double j = isnan(c->p->tm_param) ? 0.3 : c->p->tm_param;
+      if (x <= j) return x;
+      const double a = -j * j * (pk - 1.0) / (j * j - 2.0 * j + pk);
+      const double b = (j * j - 2.0 * j * pk + pk) / fmax(1e-6, pk - 1.0);
+      return (b * b + 2.0 * b * j + j * j) / (b - a) * (x + a) / (x + b);
+    }
+  }
+}
+
+/* bt2390_pq in double */
+static double bt2390_pq_d(const ocfg *c, double e1) {
+  double e1n = (e1 - c->src_min) / (c->src_max - c->src_min);
+  e1n = e1n != e1n ? 1.0 : (e1n < 0.0 ? 0.0 : (e1n > 1.0 ? 1.0 : e1n));
+  const double ks = c->ks, ml = c->max_lum;
+  double e2 = e1n;
+  if (ks < 1.0 && e1n > ks) {
+    const double t = (e1n - ks) / (1.0 - ks), t2 = t * t, t3 = t2 * t;
+    e2 = (2.0 * t3 - 3.0 * t2 + 1.0) * ks + (t3 - 2.0 * t2 + t) * (1.0 - ks) + (-2.0 * t3 + 3.0 * t2) * ml;
+  }
+  if (c->min_lum > 0.0 && e2 < 1.0) {
+    e2 += c->min_lum * pow(1.0 - e2, c->bp);
+    e2 = c->bgain * (e2 - c->min_lum) + c->min_lum;
+  }
+  return e2 * (c->src_max - c->src_min) + c->src_min;
+}
+
+/* spline_pq_f in double */
+static double spline_pq_d(const ocfg *c, double e) {
+  double x = e < c->sp_smin ? c->sp_smin : (e > c->sp_smax ? c->sp_smax : e);
+  x -= c->sp_kin;
+  double y = x > 0.0 ? ((c->sp_qa * x + c->sp_qb) * x + c->sp_qc) * x : (c->sp_pa * x + c->sp_pb) * x;
+  y += c->sp_kout;
+  return y < c->sp_dmin ? c->sp_dmin : (y > c->sp_dmax ? c->sp_dmax : y);
+}
+
+/* the branch's PQ-domain curve (IPT intensity, or the max(R,G,B) signal) */
+static double lp_curve_pq_x(const ocfg *c, double e) {
+  switch (c->p->tonemap) {
+    case H2S_TM_BT2390: return bt2390_pq_d(c, e);
+    case H2S_TM_SPLINE: return spline_pq_d(c, e);
+    default: return pq_encode_d(lp_norm_curve_d(c, pq_eotf_z(e) * (10000.0 / c->tw)) * (c->tw / 10000.0));
+  }
+}
+
+/* S2 of the branch in double (tone_ipt / tonemap_px's libplacebo forms) */
+static rgbd tone_lp_d(const ocfg *c, rgbd in) {
+  /* inputs capped at 1e6 npl in the IPT form and the NORM curves' gain (as
+   * tone_ipt / tonemap_px); BT.2390 / spline as the max(R,G,B) gain take
+   * them as they are (an infinite channel: NaN signal, clipped to the top) */
+  const int tm = c->p->tonemap, capped = c->ipt || (tm >= H2S_TM_REINHARD && tm <= H2S_TM_MOBIUS);
+  const double cap = capped ? 1e6 : (double)INFINITY;
+  rgbd v = {in.r < cap ? in.r : cap, in.g < cap ? in.g : cap, in.b < cap ? in.b : cap}, o;
+  if (c->ipt) {
+    const double s = c->p->npl / 10000.0, w[3] = {v.r * s, v.g * s, v.b * s};
+    double q[3], l[3];
+    for (int k = 0; k < 3; k++) q[k] = pq_encode_d(c->r2l[k][0] * w[0] + c->r2l[k][1] * w[1] + c->r2l[k][2] * w[2]);
+    const double I = 0.4 * q[0] + 0.4 * q[1] + 0.2 * q[2];
+    const double dI = lp_curve_pq_x(c, I) - I;
+    for (int k = 0; k < 3; k++) l[k] = pq_eotf_z(q[k] + dI);
+    const double os = c->out_scale;
+    o.r = (c->l2r[0][0] * l[0] + c->l2r[0][1] * l[1] + c->l2r[0][2] * l[2]) * os;
+    o.g = (c->l2r[1][0] * l[0] + c->l2r[1][1] * l[1] + c->l2r[1][2] * l[2]) * os;
+    o.b = (c->l2r[2][0] * l[0] + c->l2r[2][1] * l[1] + c->l2r[2][2] * l[2]) * os;
+    return o;
+  }
+  double sig = v.r > v.g ? v.r : v.g;
+  sig = sig > v.b ? sig : v.b;
+  sig = sig > 1e-6 ? sig : 1e-6;
+  double k;
+  if (tm >= H2S_TM_REINHARD && tm <= H2S_TM_MOBIUS)
+    k = lp_norm_curve_d(c, sig * (c->p->npl / c->tw)) / sig;
+  else
+    k = pq_eotf_z(lp_curve_pq_x(c, pq_encode_d(sig * (c->p->npl / 10000.0)))) * c->out_scale / sig;
+  o.r = v.r * k, o.g = v.g * k, o.b = v.b * k;
+  return o;
+}
+
+static double lp_encode_d(const ocfg *c, double x) {
+  if (!(x > 0.0)) x = 0.0;
+  return pow(x / c->enc_a, 1.0 / 2.4) - c->enc_b;
+}
+
+/* the rgba8 download's pre-rounding value (code = floor(x)) */
+static double rgba8_x(const ocfg *c, double v, int x, int y) {
+  v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+  return v * (double)c->lp_qs + ((double)c->lp_qo + (c->lp_dith ? (double)bayer16(x, y) : 0.5));
+}
+
+/* one pixel of the branch through S1..S4 (as chain_px) from its codes;
+ * xq (LUT on, may be NULL): the three download values x */
+static rgbf chain_lp_d(const ocfg *c, const h2s_frames *in, int f, int x, int y, int upto, double xq[3]) {
+  const int cw = in->width / 2, ch = in->height / 2, sh = c->p->bits_in - 8;
+  const double yv = ((double)(rd(in, 0, f, x, y) & c->in_mask) - (double)(16 << sh)) / (double)(219 << sh);
+  const double cb = upsample_d(c, in, 1, f, x, y, cw, ch), cr = upsample_d(c, in, 2, f, x, y, cw, ch);
+  const double kr = 0.2627, kb = 0.0593, kg = 1.0 - kr - kb;
+  const double er = yv + 2.0 * (1.0 - kr) * cr;
+  const double eg = yv - 2.0 * kb * (1.0 - kb) / kg * cb - 2.0 * kr * (1.0 - kr) / kg * cr;
+  const double eb = yv + 2.0 * (1.0 - kb) * cb;
+  rgbd l;
+  if (c->p->transfer_in == H2S_TRC_HLG) {
+    l.r = hlg_inv_oetf_d(er), l.g = hlg_inv_oetf_d(eg), l.b = hlg_inv_oetf_d(eb);
+    const double ys = 0.2627 * l.r + 0.6780 * l.g + 0.0593 * l.b;
+    const double w = ys > 0.0 ? 1000.0 / c->p->npl * pow(ys, 0.2) : 0.0;
+    l.r *= w, l.g *= w, l.b *= w;
+  } else {
+    const double s = 10000.0 / c->p->npl;
+    l.r = pq_eotf_z(er) * s, l.g = pq_eotf_z(eg) * s, l.b = pq_eotf_z(eb) * s;
+  }
+  rgbf o;
+  if (upto == H2S_STAGE_LINEAR) {
+    o.r = (float)l.r, o.g = (float)l.g, o.b = (float)l.b;
+    return o;
+  }
+  const rgbd t = tone_lp_d(c, l);
+  if (upto == H2S_STAGE_TONEMAP) {
+    o.r = (float)t.r, o.g = (float)t.g, o.b = (float)t.b;
+    return o;
+  }
+  if (c->p->lut_enabled) {
+    const double g[3] = {lp_encode_d(c, t.r), lp_encode_d(c, t.g), lp_encode_d(c, t.b)};
+    if (upto == H2S_STAGE_GAMMA) {
+      o.r = (float)g[0], o.g = (float)g[1], o.b = (float)g[2];
+      return o;
+    }
+    int q[3];
+    for (int k = 0; k < 3; k++) {
+      const double xv = rgba8_x(c, g[k], x, y);
+      if (xq) xq[k] = xv;
+      q[k] = (int)floor(xv) + g_lp_bias;
+      q[k] = q[k] < 0 ? 0 : (q[k] > 255 ? 255 : q[k]);
+    }
+    const rgbf r8 = lut3d_8bit(c, q[0], q[1], q[2]);
+    o.r = r8.r / 255.0f, o.g = r8.g / 255.0f, o.b = r8.b / 255.0f;
+    return o;
+  }
+  /* LUT off: libplacebo's BT.2020 -> BT.709 matrix (tools/generate_lut.py:36-40), the encode, clipped */
+  const double m[3][3] = {{1.6604910021, -0.5876411388, -0.0728498633},
+                          {-0.1245504745, 1.1328998971, -0.0083494226},
+                          {-0.0181507634, -0.1005788980, 1.1187296614}};
+  double gg[3];
+  for (int k = 0; k < 3; k++) {
+    const double v = lp_encode_d(c, m[k][0] * t.r + m[k][1] * t.g + m[k][2] * t.b);
+    gg[k] = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+  }
+  o.r = (float)gg[0], o.g = (float)gg[1], o.b = (float)gg[2];
+  return o;
+}
+
+static inline int lp_exact(const ocfg *c) { return c->pipe == H2S_PIPE_LIBPLACEBO && !g_lp_f32; }
+
 /* ---- S6 model + S7 + S8 -------------------------------------------------- */
 static const float K709_R = 0.2126f, K709_G = 0.7152f, K709_B = 0.0722f;
 
@@ -895,7 +1119,7 @@ static yuvf px_yuv(const ocfg *c, const h2s_frames *in, int f, int x, int y) {
   float yv = (float)(rd(in, 0, f, x, y) & c->in_mask) * c->y_scale + c->y_off;
   float cb = upsample(c, in, 1, f, x, y, cw, ch);
   float cr = upsample(c, in, 2, f, x, y, cw, ch);
-  rgbf o = chain_px(c, yv, cb, cr, 99, x, y);
+  rgbf o = lp_exact(c) ? chain_lp_d(c, in, f, x, y, 99, NULL) : chain_px(c, yv, cb, cr, 99, x, y);
   float R = clip01n(o.r), G = clip01n(o.g), B = clip01n(o.b);
   float Y = K709_R * R + K709_G * G + K709_B * B;
   yuvf r = {(16.0f + 219.0f * Y) * s, cbr * R + cbg * G + cbb * B, crr * R + crg * G + crb * B};
@@ -1054,6 +1278,9 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
   int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
   size_t plane = (size_t)W * H;
   const float s = (float)(1 << (c.q_bits - 8));
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
   for (int y = 0; y < H; y++)
     for (int x = 0; x < W; x++) {
       size_t i = (size_t)y * W + x;
@@ -1067,7 +1294,7 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
       float yv = (float)(rd(in, 0, 0, x, y) & c.in_mask) * c.y_scale + c.y_off;
       float cb = upsample(&c, in, 1, 0, x, y, cw, ch);
       float cr = upsample(&c, in, 2, 0, x, y, cw, ch);
-      rgbf o = chain_px(&c, yv, cb, cr, stage, x, y);
+      rgbf o = lp_exact(&c) ? chain_lp_d(&c, in, 0, x, y, stage, NULL) : chain_px(&c, yv, cb, cr, stage, x, y);
       out_rgb[i] = o.r;
       out_rgb[plane + i] = o.g;
       out_rgb[2 * plane + i] = o.b;
@@ -1083,9 +1310,17 @@ int oracle_tonemap_lin(const h2s_params *p, const float *lut, int lut_n, const f
   ocfg c;
   int rc = resolve(&c, p, lut, lut_n);
   if (rc) return rc;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
   for (int i = 0; i < n; i++) {
-    rgbf l = {in_rgb[i], in_rgb[n + i], in_rgb[2 * n + i]};
-    rgbf o = tonemap_px(&c, l);
+    rgbf l = {in_rgb[i], in_rgb[n + i], in_rgb[2 * n + i]}, o;
+    if (lp_exact(&c)) {
+      const rgbd ld = {l.r, l.g, l.b}, t = tone_lp_d(&c, ld);
+      o.r = (float)t.r, o.g = (float)t.g, o.b = (float)t.b;
+    } else {
+      o = tonemap_px(&c, l);
+    }
     out_rgb[i] = o.r;
     out_rgb[n + i] = o.g;
     out_rgb[2 * n + i] = o.b;
@@ -1120,6 +1355,34 @@ float oracle_tone_curve(const h2s_params *p, float sig) {
   rgbf in = {sig, sig, sig};
   rgbf o = tonemap_px(&c, in);
   return o.r;
+}
+
+/* the libplacebo branch's stage 1-3 form: 0 = exact (double, the default),
+ * 1 = the round-5 float32 form; and the gate mutation hook (a bias added to
+ * every rgba8 download code).  Process-wide test switches. */
+void oracle_set_lp_f32(int on) { g_lp_f32 = on != 0; }
+void oracle_set_lp_bias(int codes) { g_lp_bias = codes; }
+
+/* libplacebo branch with the LUT: the exact pre-rounding value x of each
+ * rgba8 download channel of frame 0 (code = floor(x)), planar [3][H][W];
+ * H2S_E_UNSUPPORTED on the CPU chain or with the LUT off (no rgba8 download) */
+int oracle_lp_download(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, double *out_x) {
+  ocfg c;
+  int rc = resolve(&c, p, lut, lut_n);
+  if (rc) return rc;
+  if (c.pipe != H2S_PIPE_LIBPLACEBO || !p->lut_enabled) return H2S_E_UNSUPPORTED;
+  const int W = in->width, H = in->height;
+  const size_t plane = (size_t)W * H;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      double xq[3];
+      chain_lp_d(&c, in, 0, x, y, H2S_STAGE_LUT, xq);
+      for (int k = 0; k < 3; k++) out_x[k * plane + (size_t)y * W + x] = xq[k];
+    }
+  return 0;
 }
 
 float oracle_pq_eotf(float x) { return st2084_eotf(x); }

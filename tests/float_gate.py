@@ -131,15 +131,16 @@ class Tolerance:
     pass
 
 
-def _stage2_spread(params, P, U1):
+def _stage2_spread(params, P, U1, lin=None):
     """sum_k |J[c, k]| U1[k]: the stage-1 uncertainty U1 (3, H, W) carried
     through the chain's tone map, J its Jacobian at the oracle's stage-1
     values by central differences of the oracle's own S2 (oracle.tonemap_lin;
     steps of 1e-3 relative, so float32 noise stays far below the tolerance).
     This is what desaturation's luma mixing (kappa), the tone gain and, on
     the libplacebo branch, the IPT rows and the black-point lift do to an
-    input disagreement -- per channel, not the pixel's largest channel."""
-    lin = np.nan_to_num(P[1], nan=0.0, posinf=0.0).astype(np.float64)
+    input disagreement -- per channel, not the pixel's largest channel.
+    lin: the stage-1 values to take it at (any (3, ...) subset of P[1])."""
+    lin = np.nan_to_num(P[1] if lin is None else lin, nan=0.0, posinf=0.0).astype(np.float64)
     out = np.zeros(lin.shape)
     lat = lattice(P.lut_n) if params.lut_enabled else None
     for k in range(3):
@@ -153,6 +154,53 @@ def _stage2_spread(params, P, U1):
             J = np.nan_to_num((fh - fl) / (hi[k] - lo[k])[None], nan=0.0, posinf=0.0, neginf=0.0)
         out += np.abs(J) * U1[k][None]
     return out
+
+
+def lp_stage3_bound(params, kernel, P, ys, xs):
+    """The stated error bound of a kernel's libplacebo-branch stage-3 value
+    (the BT.1886-encoded R'G'B' the 8-bit rgba download rounds), per channel
+    at the pixels (ys, xs) of P's frame, in units of that value ([0, 1]):
+    the float gate's own propagation (float_tolerance's U at stage 3 -- the
+    EOTF's conditioning at stage 1 carried through the tone map's Jacobian,
+    the tone curve's cancellation, on k_tile's IPT form EPS_IPT through the
+    LMS -> RGB rows, then the encode's slope) plus the float32 encode's own
+    rounding (v_log_f32 / v_exp_f32 or powf: a few ulp of the exponent
+    log2(x) / 2.4 and of the result).  kernel: 'k_tile', 'generic' (a float32
+    restatement: the round-5 oracle form), or 'exact' (double arithmetic:
+    the generic kernel's libplacebo path, H2S_OPT_LP_EXACT).  Returns (3, n)."""
+    from ipt_cond import ipt_channel_scale, lp_encode_spread, stage1_uncertainty
+    n = len(ys)
+    t2 = np.nan_to_num(P[2][:, ys, xs]).reshape(3, 1, n)
+    t3 = np.nan_to_num(P[3][:, ys, xs]).reshape(3, 1, n)
+    if kernel == 'exact':
+        return (1e-12 * (1.0 + np.abs(t3))).reshape(3, n)
+    lin = np.nan_to_num(P[1][:, ys, xs], nan=0.0, posinf=0.0).reshape(3, 1, n)
+    # stage1_uncertainty / tone_uncertainty bound the disagreement of TWO
+    # float32 evaluations; against exact arithmetic a float32 kernel carries
+    # one of them: half
+    U = 0.5 * stage1_uncertainty(lin, params.npl, params.transfer)
+    U = _stage2_spread(params, P, U, lin=lin) + 0.5 * tone_uncertainty(params, P.op)
+    if kernel == 'k_tile' and params.lp_tone == 'ipt':
+        U = U + EPS_IPT * ipt_channel_scale(t2)
+    if params.lp_tone == 'max-rgb' and params.tonemapper in ('bt.2390', 'spline'):
+        # the gain's own EOTF: s2 = EOTF(curve(PQ(sig))) is a second float32
+        # decode, with the EOTF's conditioning at the curve's output (the
+        # stage-1 model at s2), scaling every channel alike (c s2 / sig)
+        tw_ = 203.0 if params.target_white != params.target_white else params.target_white
+        s2 = np.max(np.abs(t2), axis=0, keepdims=True) * tw_ / params.npl      # units of npl
+        with np.errstate(divide='ignore', invalid='ignore'):
+            rel = np.nan_to_num(0.5 * stage1_uncertainty(np.repeat(s2, 3, axis=0), params.npl, 'pq')[:1] / s2,
+                                nan=0.0, posinf=0.0)
+        U = U + rel * np.abs(t2)
+    U3 = lp_encode_spread(params, t2, U)
+    tw = 203.0 if params.target_white != params.target_white else params.target_white
+    tb = tw / 1000.0 if params.target_black != params.target_black else params.target_black
+    lb = (tb / tw) ** (1 / 2.4)
+    a, b = (1 - lb) ** 2.4, lb / (1 - lb)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        l2 = np.abs(np.nan_to_num(np.log2(np.maximum(t2, 1e-30) / a), posinf=0.0, neginf=0.0))
+    enc = 2.0 ** -21 * (np.abs(t3) + b) * (1.0 + l2)
+    return np.nan_to_num(U3 + enc, nan=0.0, posinf=0.0).reshape(3, n)
 
 
 def float_tolerance(params, kernel, stage, kind, P):
