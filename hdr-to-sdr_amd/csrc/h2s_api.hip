@@ -303,6 +303,7 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
     k->mob_k = (b * b + 2.0f * b * j + j * j) / (b - a);
   }
   k->peak = peak;
+  k->x_peak = peak, k->x_avg = 0.0, k->x_npl = p->npl, k->x_tm_param = p->tm_param, k->x_sh = p->bits_in - 8;
   // pipeline and SDR target (oracle resolve: the CPU chain's curve output is
   // relative to npl with no black; libplacebo targets PL_COLOR_SDR_WHITE =
   // 203 nits at PL_COLOR_SDR_CONTRAST = 1000:1)
@@ -1498,7 +1499,7 @@ static h2s_frames frames_at(const h2s_frames* f, int start) {
 // descriptors for frame 0.
 static int process_pipelined(h2s_ctx* c, KParams k, const h2s_frames* in, const h2s_frames* out,
                              const h2s_frames& din, const h2s_frames& dout, int nframes, bool fast, bool vec,
-                             bool out8, hipStream_t s) {
+                             bool out8, hipStream_t s, bool dyn_peak) {
   const bool host_in = in->location == H2S_LOC_HOST, host_out = out->location == H2S_LOC_HOST;
   for (hipStream_t& ps : c->ps)
     if (!ps) {
@@ -1543,8 +1544,15 @@ static int process_pipelined(h2s_ctx* c, KParams k, const h2s_frames* in, const 
       hipEventRecord(c->ev0[slot], s_cmp);
     }
     fill_geometry(&k, &ci, &co, nf);
-    if ((e = launch_chain(c, k, fast, vec, out8, nf, s_cmp)) != hipSuccess) what = "kernel launch";
-    else if (host_out) {
+    if (dyn_peak) {
+      if (int rc = run_dynamic_peak(c, k, fast, vec, out8, nf, s_cmp)) {
+        for (hipStream_t ps : c->ps) hipStreamSynchronize(ps);
+        return rc;
+      }
+    } else if ((e = launch_chain(c, k, fast, vec, out8, nf, s_cmp)) != hipSuccess) {
+      what = "kernel launch";
+    }
+    if (!what && host_out) {
       const h2s_frames ho = frames_at(out, f0);
       if ((e = hipEventRecord(c->pev[kMaxChunks + i], s_cmp)) != hipSuccess) what = "pipeline event";
       else if ((e = hipStreamWaitEvent(s_out, c->pev[kMaxChunks + i], 0)) != hipSuccess) what = "pipeline ordering";
@@ -1630,10 +1638,11 @@ int h2s_process(h2s_ctx* c, const h2s_frames* in, const h2s_frames* out, int nfr
   }
   const bool dyn_peak = c->params.peak_detect &&
                         (k.tonemap == H2S_TM_BT2390 || k.tonemap == H2S_TM_SPLINE || k.pipe == h2s::PIPE_LIBPLACEBO);
-  // the dynamic peak walks frames in order with a host round trip per frame,
-  // so it keeps the serial schedule
-  if ((host_in || host_out) && nframes > 1 && !dyn_peak && !c->serial_host)
-    return process_pipelined(c, k, in, out, din, dout, nframes, fast, vec, out8, s);
+  // host frames: the chunk pipeline, with the dynamic peak too (its
+  // statistics, IIR and curve records run on the device, stream-ordered per
+  // chunk on the compute stream, so the state still advances frame by frame)
+  if ((host_in || host_out) && nframes > 1 && !c->serial_host)
+    return process_pipelined(c, k, in, out, din, dout, nframes, fast, vec, out8, s, dyn_peak);
   if (host_in) {
     hipError_t e = copy_frames(&din, in, nframes, s);
     if (e != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "host->device copy"));
@@ -1748,6 +1757,8 @@ int h2s_set_option(h2s_ctx* c, int key, int64_t value) {
     case H2S_OPT_LP_EXACT:
       c->lp_exact = value != 0;
       return 0;
+    case 4:   // reserved: H2S_OPT_LP_EXACT's key in ABI 3.3
+      return fail(c, H2S_E_INVALID_ARG, "option 4 is reserved (H2S_OPT_LP_EXACT is option 5 since ABI 3.4)");
     case H2S_OPT_TEST_FAIL_AFTER_LAUNCH:
       c->fail_after_launch = value != 0;
       return 0;
@@ -1920,14 +1931,21 @@ int h2s_preview_rgb24_batch(h2s_ctx* c, const h2s_frames* in, int nframes, uint8
     const size_t pb = sizeof(h2s::PeakState);
     hipError_t e = hipMemcpyAsync(c->d_pk + 1, c->d_pk, pb, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return hip_fail(c, e, "peak state save");
+    // every exit after the save queues the restore first (best effort)
+    auto restored = [&](int code) {
+      (void)hipMemcpyAsync(c->d_pk, c->d_pk + 1, pb, hipMemcpyDeviceToDevice, s);
+      (void)peak_done(c, s);
+      return code;
+    };
     for (int f = 0; f < nframes; f++) {
       h2s_frames fi = *in, fo = y8;
       for (int k = 0; k < 3; k++) {
         fi.data[k] = (uint8_t*)in->data[k] + (long long)f * in->frame_pitch[k];
         fo.data[k] = (uint8_t*)y8.data[k] + (long long)f * y8.frame_pitch[k];
       }
-      if ((e = hipMemsetAsync(c->d_pk, 0, pb, s)) != hipSuccess) return queued_exit(c, s, hip_fail(c, e, "peak state reset"));
-      if ((rc = h2s_process(c, &fi, &fo, 1, hip_stream))) return rc;
+      if ((e = hipMemsetAsync(c->d_pk, 0, pb, s)) != hipSuccess)
+        return restored(queued_exit(c, s, hip_fail(c, e, "peak state reset")));
+      if ((rc = h2s_process(c, &fi, &fo, 1, hip_stream))) return restored(rc);
     }
     if ((e = hipMemcpyAsync(c->d_pk, c->d_pk + 1, pb, hipMemcpyDeviceToDevice, s)) != hipSuccess)
       return queued_exit(c, s, hip_fail(c, e, "peak state restore"));

@@ -91,6 +91,11 @@ struct KParams {
   // dynamic peak detection (one frame per launch): the frame's curve record,
   // written on the device by k_peak_curves; null: the constants above
   const CurveConsts* cv;
+  // the libplacebo branch's exact path (h2s_lpx.h): source peak (units of 100
+  // nits) and average PQ level (0: the default spline knee) its double
+  // constants derive from, npl, tm_param (NaN: default), bits_in - 8
+  double x_peak, x_avg, x_npl, x_tm_param;
+  int x_sh;
 };
 
 constexpr int PIPE_CPU = 1, PIPE_LIBPLACEBO = 2;
@@ -122,6 +127,10 @@ struct CurveConsts {
   float b_bk_a, b_bk_b, b_bk_c, b_bk_d;
   // libplacebo reinhard / hable / mobius in NORM units (1 = target white)
   float n_peak, n_rein_off, n_rein_scale, n_hable_inv, n_mob_j, n_mob_a, n_mob_b, n_mob_scale;
+  // the frame's source peak (units of 100 nits) and smoothed average PQ level,
+  // from which the generic kernel's exact libplacebo path (h2s_lpx.h) derives
+  // its double constants
+  double x_peak, x_avg;
 };
 
 // a frame's curve record over the generic kernel's constants (dynamic peak)
@@ -133,6 +142,7 @@ __device__ __forceinline__ void apply_curve(KParams& P, const CurveConsts& C) {
   P.sp_dmin = C.sp_dmin, P.sp_dmax = C.sp_dmax;
   P.n_peak = C.n_peak, P.n_rein_off = C.n_rein_off, P.n_rein_scale = C.n_rein_scale, P.n_hable_inv = C.n_hable_inv;
   P.n_mob_j = C.n_mob_j, P.n_mob_a = C.n_mob_a, P.n_mob_b = C.n_mob_b, P.n_mob_scale = C.n_mob_scale;
+  P.x_peak = C.x_peak, P.x_avg = C.x_avg;
 }
 
 // Parameters of the specialised fast kernel (h2s_fast.hip): the same chain
@@ -247,7 +257,11 @@ __device__ __forceinline__ float fpow(float x, float p) { return fexp2(p * flog2
 // branch's 8-bit rgba rounding.  The generic kernel is the branch's exact
 // path (H2S_OPT_LP_EXACT; h2s_kernels.hip is built without FMA contraction, in
 // the oracle's operation order); the tile kernel keeps its own fast forms.
+// (no FMA contraction inside: the forms round where glibc's do, whichever
+// translation unit includes them; tests/test_libm_tables.py checks the device
+// forms bit for bit against the libm through h2stest_libm)
 __device__ __forceinline__ float libm_exp2_tail(double xd, double shift, const double* C) {
+#pragma clang fp contract(off)
   double kd = xd + shift;
   const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
   kd -= shift;
@@ -262,6 +276,7 @@ __device__ __forceinline__ float libm_exp2_tail(double xd, double shift, const d
 }
 // powf for x >= 0 (the chain's uses); other bases take the double form
 __device__ __forceinline__ float libm_powf(float x, float yf) {
+#pragma clang fp contract(off)
   if (!(x > 0.0f) || !(x < __builtin_inff()) || yf == 0.0f || !(fabsf(yf) < __builtin_inff()))
     return (float)pow((double)x, (double)yf);
   unsigned ix = __float_as_uint(x);

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "h2s_device.h"
+#include "h2s_lpx.h"
 #include "h2s_peak.h"
 
 namespace h2s {
@@ -32,13 +33,17 @@ __device__ __forceinline__ int ld16(const uint8_t* row, int x) {
 // C444: BICUBIC chroma (two-pass path): store every pixel's (Cb, Cr) into
 // P.chr444 (frame 0 of the launch, W x H) instead of the 2x2 mean; the
 // chroma planes are then written by k_chroma_bicubic
-template <int QPT, bool VEC, bool OUT8, bool C444 = false, bool DYN = false>
+// LPX: the libplacebo branch, stages 1-3 in exact arithmetic (h2s_lpx.h)
+// from the integer codes (cc*: the chroma codes kept for it)
+template <int QPT, bool VEC, bool OUT8, bool C444 = false, bool DYN = false, bool LPX = false>
 __global__ __launch_bounds__(256) void k_process(const KParams P0) {
+  LpX X;
   auto body = [&](const KParams& P, const int f, const int cy, const int cx0) {
   const int cw = P.cw, ch = P.ch;
 
   // ---- chroma: rows cy-1, cy, cy+1; columns cx0 .. cx0+QPT (halo) ----
   float cu[3][QPT + 1], cv[3][QPT + 1];
+  int ccu[3][QPT + 1], ccv[3][QPT + 1];
   const int crow[3] = {edge(P, cy - 1, ch), cy, edge(P, cy + 1, ch)};
   const bool full = cx0 + QPT <= cw;
 #pragma unroll
@@ -55,17 +60,19 @@ __global__ __launch_bounds__(256) void k_process(const KParams P0) {
       int sv[5] = {(int)(b.x & 0xffff) & m, (int)(b.x >> 16) & m, (int)(b.y & 0xffff) & m, (int)(b.y >> 16) & m,
                    ld16(rv, hx) & m};
 #pragma unroll
-      for (int k = 0; k <= QPT; k++) {
-        cu[i][k] = (float)su[k] * P.c_scale + P.c_off;
-        cv[i][k] = (float)sv[k] * P.c_scale + P.c_off;
-      }
+      for (int k = 0; k <= QPT; k++) ccu[i][k] = su[k], ccv[i][k] = sv[k];
     } else {
 #pragma unroll
       for (int k = 0; k <= QPT; k++) {
         const int x = edge(P, cx0 + k, cw);
-        cu[i][k] = (float)(ld16(ru, x) & (int)P.in_mask) * P.c_scale + P.c_off;
-        cv[i][k] = (float)(ld16(rv, x) & (int)P.in_mask) * P.c_scale + P.c_off;
+        ccu[i][k] = ld16(ru, x) & (int)P.in_mask;
+        ccv[i][k] = ld16(rv, x) & (int)P.in_mask;
       }
+    }
+#pragma unroll
+    for (int k = 0; k <= QPT; k++) {
+      cu[i][k] = (float)ccu[i][k] * P.c_scale + P.c_off;
+      cv[i][k] = (float)ccv[i][k] * P.c_scale + P.c_off;
     }
   }
   // horizontal pass (left siting): h[2k] = c[k], h[2k+1] = (c[k] + c[k+1]) / 2
@@ -116,7 +123,18 @@ __global__ __launch_bounds__(256) void k_process(const KParams P0) {
       const float yv = (float)ys[j][x] * P.y_scale + P.y_off;
       float r, g, b;
       const int px = 2 * (cx0 + k) + (p & 1), py = 2 * cy + j;
-      chain_px<4>(P, yv, cb, cr, r, g, b, lp_qoff(P, px, py));
+      if (LPX) {
+        // the oracle's upsample_d: horizontal (left siting) then vertical, in double
+        auto hx = [&](const int (&c)[3][QPT + 1], int i) -> double {
+          const double a = lpx_chroma(P, c[i][x >> 1]);
+          return (x & 1) ? 0.5 * (a + lpx_chroma(P, c[i][(x >> 1) + 1])) : a;
+        };
+        const double cbd = j == 0 ? 0.25 * hx(ccu, 0) + 0.75 * hx(ccu, 1) : 0.75 * hx(ccu, 1) + 0.25 * hx(ccu, 2);
+        const double crd = j == 0 ? 0.25 * hx(ccv, 0) + 0.75 * hx(ccv, 1) : 0.75 * hx(ccv, 1) + 0.25 * hx(ccv, 2);
+        lpx_chain<4>(P, X, lpx_luma(P, ys[j][x]), cbd, crd, px, py, r, g, b);
+      } else {
+        chain_px<4>(P, yv, cb, cr, r, g, b, lp_qoff(P, px, py));
+      }
       r = clamp01(r), g = clamp01(g), b = clamp01(b);
       const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
       cbs[p] = P.kcb[0] * r + P.kcb[1] * g + P.kcb[2] * b;
@@ -200,6 +218,7 @@ __global__ __launch_bounds__(256) void k_process(const KParams P0) {
   // (P0.cv), not from the launch parameters
   KParams P = P0;
   if (DYN) apply_curve(P, *P0.cv);
+  if (LPX) X = lpx_consts(P, P.x_peak, P.x_avg);
   const long long lb = xcd_remap(blockIdx.x, gridDim.x);
   const long long item = lb * 256 + threadIdx.x;
   if (item >= P.total) return;
@@ -232,9 +251,27 @@ __global__ __launch_bounds__(256) void k_debug(const KParams P, float* out) {
     return 0.75f * hpass(plane, m) + 0.25f * hpass(plane, m + 1);
   };
   const float cb = up(1), cr = up(2);
-  const float yv = (float)(ld16(P.in[0] + y * P.in_ls[0], x) & (int)P.in_mask) * P.y_scale + P.y_off;
+  const int ycode = ld16(P.in[0] + y * P.in_ls[0], x) & (int)P.in_mask;
+  const float yv = (float)ycode * P.y_scale + P.y_off;
   float r, g, b;
-  chain_px<STAGE < 5 ? STAGE : 4>(P, yv, cb, cr, r, g, b, lp_qoff(P, x, y));
+  if (P.pipe == PIPE_LIBPLACEBO) {   // the exact path (h2s_lpx.h), as k_process<..., LPX>
+    auto hpd = [&](int plane, int cyy) -> double {
+      const uint8_t* row = P.in[plane] + edge(P, cyy, ch) * P.in_ls[plane];
+      const int k = x >> 1;
+      const double a = lpx_chroma(P, ld16(row, edge(P, k, cw)) & (int)P.in_mask);
+      if (!(x & 1)) return a;
+      return 0.5 * (a + lpx_chroma(P, ld16(row, edge(P, k + 1, cw)) & (int)P.in_mask));
+    };
+    auto upd = [&](int plane) -> double {
+      const int m = y >> 1;
+      if (!(y & 1)) return 0.25 * hpd(plane, m - 1) + 0.75 * hpd(plane, m);
+      return 0.75 * hpd(plane, m) + 0.25 * hpd(plane, m + 1);
+    };
+    const LpX X = lpx_consts(P, P.x_peak, P.x_avg);
+    lpx_chain<STAGE < 5 ? STAGE : 4>(P, X, lpx_luma(P, ycode), upd(1), upd(2), x, y, r, g, b);
+  } else {
+    chain_px<STAGE < 5 ? STAGE : 4>(P, yv, cb, cr, r, g, b, lp_qoff(P, x, y));
+  }
   if (STAGE == 5) {  // S6 quantiser inputs (oracle px_yuv)
     r = clamp01(r), g = clamp01(g), b = clamp01(b);
     const float Y = P.k709[0] * r + P.k709[1] * g + P.k709[2] * b;
@@ -292,6 +329,19 @@ hipError_t launch_process(const KParams& P, bool vec, bool out8, hipStream_t s) 
   const long long nb = (P.total + 255) / 256;
   if (nb == 0) return hipSuccess;
   dim3 grid((unsigned)nb), block(256);
+  if (P.pipe == PIPE_LIBPLACEBO) {   // the libplacebo branch's exact path (h2s_lpx.h)
+    if (P.cv) {
+      if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, false, true, true>), grid, block, 0, s, P);
+      else hipLaunchKernelGGL((k_process<QPT, false, false, false, true, true>), grid, block, 0, s, P);
+    } else if (vec) {
+      if (out8) hipLaunchKernelGGL((k_process<QPT, true, true, false, false, true>), grid, block, 0, s, P);
+      else hipLaunchKernelGGL((k_process<QPT, true, false, false, false, true>), grid, block, 0, s, P);
+    } else {
+      if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, false, false, true>), grid, block, 0, s, P);
+      else hipLaunchKernelGGL((k_process<QPT, false, false, false, false, true>), grid, block, 0, s, P);
+    }
+    return hipGetLastError();
+  }
   if (P.cv) {   // dynamic peak: the frame's curve record on the device
     if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, false, true>), grid, block, 0, s, P);
     else hipLaunchKernelGGL((k_process<QPT, false, false, false, true>), grid, block, 0, s, P);
@@ -324,6 +374,17 @@ hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s) {
   constexpr int QPT = 4;
   const long long nb = (P.total + 255) / 256;
   if (nb == 0) return hipSuccess;
+  if (P.pipe == PIPE_LIBPLACEBO) {   // the libplacebo branch's exact path (h2s_lpx.h)
+    if (P.cv) {
+      if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+      else hipLaunchKernelGGL((k_process<QPT, false, false, true, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    } else if (out8) {
+      hipLaunchKernelGGL((k_process<QPT, false, true, true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    } else {
+      hipLaunchKernelGGL((k_process<QPT, false, false, true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
+    }
+    return hipGetLastError();
+  }
   if (P.cv) {   // dynamic peak: the frame's curve record on the device
     if (out8) hipLaunchKernelGGL((k_process<QPT, false, true, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
     else hipLaunchKernelGGL((k_process<QPT, false, false, true, true>), dim3((unsigned)nb), dim3(256), 0, s, P);
@@ -503,7 +564,9 @@ __device__ void peak_curves_body(double2* fstat, int n, const PeakModel& M, Peak
 // its histogram for the next call); the last frame to finish (a device-scope
 // counter after a release fence: one per frame, so the fences stay few) runs
 // the IIR and the curve records for all of the launch's frames.  PeakTail
-// (h2s_peak.h) names the buffers; the counter is zero on entry and left zero.
+// (h2s_peak.h) names the buffers; the counter is zeroed by the statistics
+// launch queued before every finish launch (so an aborted launch cannot
+// leave it stale) and left zero.
 __global__ __launch_bounds__(256) void k_peak_finish(const float2* partial, const PeakTail T) {
   const int f = blockIdx.x;
   __shared__ int s_last;
@@ -524,6 +587,7 @@ __global__ __launch_bounds__(256) void k_peak_finish(const float2* partial, cons
 template <int TRC, bool HIST>
 __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* partial, const PeakTail T) {
   __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *T.done = 0u;   // k_peak_finish's counter (stream-ordered)
   if (HIST)
     for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
   if (HIST) __syncthreads();
@@ -563,6 +627,7 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
 template <int TRC, bool HIST, bool ROW2 = false>
 __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, const PeakTail T) {
   __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *T.done = 0u;   // k_peak_finish's counter (stream-ordered)
   if (HIST)
     for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
   if (HIST) __syncthreads();
@@ -701,4 +766,32 @@ hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakSta
   return hipGetLastError();
 }
 
+// device libm_powf / libm_expf over n inputs (fn 0: powf(x, y), 1: expf(x)),
+// for tests/test_libm_tables.py's bit-equality check against the libm the
+// oracle links
+__global__ void k_test_libm(int fn, const float* x, const float* y, float* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = fn == 0 ? libm_powf(x[i], y[i]) : libm_expf(x[i]);
+}
+
 }  // namespace h2s
+
+// Private test entry (not part of the C-ABI, not declared in include/h2s.h):
+// host arrays in and out, synchronous, on the current device.  Returns 0 or
+// a negative HIP error.
+extern "C" __attribute__((visibility("default"))) int h2stest_libm(int fn, const float* x, const float* y, float* out,
+                                                                    int n) {
+  if (n <= 0) return 0;
+  float* d = nullptr;
+  const size_t b = (size_t)n * sizeof(float);
+  if (hipMalloc(&d, 3 * b) != hipSuccess) return -1;
+  hipError_t e = hipMemcpy(d, x, b, hipMemcpyHostToDevice);
+  if (e == hipSuccess && y) e = hipMemcpy(d + n, y, b, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(h2s::k_test_libm, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, d, d + n, d + 2 * n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, b, hipMemcpyDeviceToHost);
+  hipFree(d);
+  return e == hipSuccess ? 0 : -(int)e;
+}

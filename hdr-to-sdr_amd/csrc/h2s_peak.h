@@ -221,6 +221,7 @@ __host__ __device__ inline void curve_for_peak(const PeakModel& m, double peak, 
   else if (m.family == 8) spline_consts(peak, avg_pq, m.contrast, m.t_white, m.t_black, &plain, m.pq);
   else lp_norm_consts(peak, m.tm_param, m.t_white, &plain);
   curve_fast(plain, cc);
+  cc->x_peak = peak, cc->x_avg = avg_pq;
 }
 
 // the frame's peak (units of 100 nits, as vf_tonemap's peak) from the

@@ -38,7 +38,8 @@ LP_RANGE_FULL, LP_RANGE_LIMITED = 0, 1
 LP_DITHER_NONE, LP_DITHER_ORDERED = 0, 1
 LP_P010_KEEP, LP_P010_TRUNCATE = 0, 1
 PIPE_AUTO, PIPE_CPU_CHAIN, PIPE_LIBPLACEBO = 0, 1, 2
-OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL, OPT_LP_EXACT = 1, 2, 3, 4
+OPT_FAST_PATH, OPT_TILES_PER_BLOCK, OPT_HOST_SERIAL, OPT_LP_EXACT = 1, 2, 3, 5
+OPT_RESERVED_4 = 4   # H2S_OPT_LP_EXACT's key in ABI 3.3: now INVALID_ARG
 # private test hook (include/h2s.h H2S_PRIVATE_TEST_HOOKS: not part of the ABI)
 OPT_TEST_FAIL_AFTER_LAUNCH = 0x7f000000 + 1
 OPT_TEST_PEAK_FORM = 0x7f000000 + 2
@@ -46,7 +47,7 @@ OPT_TEST_PEAK_CHUNK = 0x7f000000 + 3
 OPT_TEST_PEAK_BLOCKS = 0x7f000000 + 4
 PATH_TILE, PATH_TILE_TAIL, PATH_GENERIC, PATH_TWO_PASS = 1, 2, 3, 4
 ABI_VERSION = 3
-ABI_MINOR = 3   # include/h2s.h H2S_ABI_MINOR (the loaded library may be newer, not older)
+ABI_MINOR = 4   # include/h2s.h H2S_ABI_MINOR (the loaded library may be newer, not older)
 
 # every symbol include/h2s.h declares (checked by tests/test_abi_exports.py)
 EXPORTS = (

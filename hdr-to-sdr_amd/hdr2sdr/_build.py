@@ -22,7 +22,7 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, 'build', 'liboracle.so')
 ARCH = os.environ.get('H2S_OFFLOAD_ARCH', 'gfx950')
 SOURCES = ['h2s_fast_dbg345.hip', 'h2s_fast_dbg12.hip', 'h2s_fast_lp.hip', 'h2s_fast.hip', 'h2s_api.hip', 'h2s_kernels.hip',
            'h2s_preview.hip', 'h2s_cube.cpp']
-HEADERS = ['h2s_device.h', 'h2s_tile.h', 'h2s_peak.h', 'h2s_libm.h']
+HEADERS = ['h2s_device.h', 'h2s_tile.h', 'h2s_peak.h', 'h2s_libm.h', 'h2s_lpx.h']
 
 
 def _hipcc() -> str:

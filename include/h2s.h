@@ -51,8 +51,12 @@ extern "C" {
  *      h2s_peak_state / _reset / _feed wait for the context's queued work; a
  *      preview restores the context's peak state; the failure-injection test
  *      hook moved to the private option range (H2S_PRIVATE_TEST_HOOKS);
- *   3: H2S_OPT_LP_EXACT. */
-#define H2S_ABI_MINOR 3
+ *   3: H2S_OPT_LP_EXACT (then key 4);
+ *   4: H2S_OPT_LP_EXACT moves to key 5 and key 4 is reserved (H2S_E_INVALID_ARG:
+ *      a 3.0 / 3.1 client that set key 4 as the old failure-injection hook
+ *      fails loudly instead of switching kernels); the libplacebo branch's
+ *      exact path computes stages 1-3 in double precision (see below). */
+#define H2S_ABI_MINOR 4
 
 /* ---- error codes ------------------------------------------------------- */
 #define H2S_OK 0
@@ -201,17 +205,19 @@ enum h2s_option {
   H2S_OPT_FAST_PATH = 1,       /* 1 (default): the tile kernel where it applies; 0: generic kernel only */
   H2S_OPT_TILES_PER_BLOCK = 2, /* tile kernel: 64x32 tiles one block walks (1..64, default 8)          */
   H2S_OPT_HOST_SERIAL = 3,     /* host frames: 1 = one H2D, kernel, D2H per call (no chunk pipeline)   */
-  H2S_OPT_LP_EXACT = 4         /* 1: the libplacebo branch on the generic kernel only (see below)       */
+  /* 4: reserved (H2S_E_INVALID_ARG; was H2S_OPT_LP_EXACT in ABI 3.3)                                  */
+  H2S_OPT_LP_EXACT = 5         /* 1: the libplacebo branch on its exact path only (see below)           */
 };
 /* H2S_OPT_LP_EXACT: the libplacebo branch's 8-bit rgba download rounds a
- * float (255 x the BT.1886 encode) whose IPT tone-mapping form is ill
- * conditioned in float32; the tile kernel (default) lands within its table
- * error of the reference's value and so may round a near-tie code the other
- * way (0.1 % of codes; the lut3d's 8-bit lattice step then spreads the flip
- * over a few output steps).  With 1 the branch runs on the generic kernel,
- * which follows the reference's operation order with correctly rounded
- * powers and keeps the IPT form in double: output within one step of the
- * reference's, at about 4x the tile kernel's time. */
+ * float (255 x the BT.1886 encode).  The reference computes it in
+ * libplacebo's float32 GLSL, so the restated reference is exact arithmetic;
+ * the tile kernel (default, float32) lands within its stated error bound of
+ * it and may round a code lying that close to a tie the other way (about
+ * 0.1 % of codes; lut3d's 8-bit lattice step then spreads such a flip over a
+ * few output steps).  With 1 the branch runs on the generic kernel's exact
+ * path, stages 1-3 in double precision from the integer codes: output within
+ * one step of the restated reference everywhere, at a multiple of the tile
+ * kernel's time. */
 /* Keys from H2S_OPT_PRIVATE_BASE up are the library's own test / debug hooks:
  * not part of the ABI, may change or vanish in any build. */
 #define H2S_OPT_PRIVATE_BASE 0x7f000000

@@ -108,6 +108,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_process_knee.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
                                           ctypes.POINTER(Frames), ctypes.POINTER(Frames), ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double]
+        L.oracle_debug_float_knee.restype = ctypes.c_int
+        L.oracle_debug_float_knee.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.POINTER(Frames), ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
+        L.oracle_tonemap_lin_knee.restype = ctypes.c_int
+        L.oracle_tonemap_lin_knee.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
         L.oracle_debug_float.restype = ctypes.c_int
         L.oracle_debug_float.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
                                          ctypes.POINTER(Frames), ctypes.c_int, ctypes.c_void_p]
@@ -134,7 +140,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_set_lp_bias.argtypes = [ctypes.c_int]
         L.oracle_lp_download.restype = ctypes.c_int
         L.oracle_lp_download.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_int,
-                                         ctypes.POINTER(Frames), ctypes.c_void_p]
+                                         ctypes.POINTER(Frames), ctypes.c_double, ctypes.c_void_p]
         L.oracle_preview_tail.restype = ctypes.c_int
         L.oracle_preview_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
@@ -180,21 +186,21 @@ def process(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width
 
 
 def debug_float(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
-                stage: int) -> np.ndarray:
+                stage: int, avg_pq: float = 0.0) -> np.ndarray:
     out = np.empty((3, height, width), dtype=np.float32)
     din = _frames(np.ascontiguousarray(buf[:1]), width, height, params.bits_in)
     lat, n = (None, 0)
     if lattice is not None:
         lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
         n = round(lat.shape[0] ** (1 / 3))
-    rc = lib().oracle_debug_float(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
-                                  ctypes.byref(din), stage, out.ctypes.data)
+    rc = lib().oracle_debug_float_knee(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                                       ctypes.byref(din), stage, float(avg_pq), out.ctypes.data)
     if rc:
         raise ValueError(f'oracle_debug_float failed: {rc}')
     return out
 
 
-def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray) -> np.ndarray:
+def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray, avg_pq: float = 0.0) -> np.ndarray:
     """S2 alone (the chain's tone map, oracle tonemap_px) on linear R'G'B'
     planes rgb[3, ...] in units of npl; float32 like the chain."""
     shp = rgb.shape
@@ -204,14 +210,15 @@ def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray) -
     if lattice is not None:
         lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
         n = round(lat.shape[0] ** (1 / 3))
-    rc = lib().oracle_tonemap_lin(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
-                                  a.ctypes.data, a.shape[1], out.ctypes.data)
+    rc = lib().oracle_tonemap_lin_knee(ctypes.byref(params), lat.ctypes.data if lat is not None else None, n,
+                                       a.ctypes.data, a.shape[1], float(avg_pq), out.ctypes.data)
     if rc:
         raise ValueError(f'oracle_tonemap_lin failed: {rc}')
     return out.reshape(shp)
 
 
-def lp_download(params: Params, lattice: np.ndarray, buf: np.ndarray, width: int, height: int) -> np.ndarray:
+def lp_download(params: Params, lattice: np.ndarray, buf: np.ndarray, width: int, height: int,
+                avg_pq: float = 0.0) -> np.ndarray:
     """libplacebo branch with the LUT: the exact (double) pre-rounding value x
     of every rgba8 download channel of frame 0, [3, H, W] float64; the code is
     floor(x).  The tie attribution of tests/lp_gate.py reads it."""
@@ -219,7 +226,8 @@ def lp_download(params: Params, lattice: np.ndarray, buf: np.ndarray, width: int
     din = _frames(np.ascontiguousarray(buf[:1]), width, height, params.bits_in)
     lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
     n = round(lat.shape[0] ** (1 / 3))
-    rc = lib().oracle_lp_download(ctypes.byref(params), lat.ctypes.data, n, ctypes.byref(din), out.ctypes.data)
+    rc = lib().oracle_lp_download(ctypes.byref(params), lat.ctypes.data, n, ctypes.byref(din), float(avg_pq),
+                                  out.ctypes.data)
     if rc:
         raise ValueError(f'oracle_lp_download failed: {rc}')
     return out
@@ -333,10 +341,12 @@ class PeakState:
 
 
 def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarray, width: int, height: int,
-                    state: 'PeakState | None' = None) -> 'tuple[np.ndarray, list[float]]':
+                    state: 'PeakState | None' = None, knees: 'list | None' = None) -> 'tuple[np.ndarray, list[float]]':
     """BT.2390 / spline with the detected peak: stats, smoothing, then each
     frame through the chain with its own peak (and, for spline, the smoothed
-    average as the knee source).  Returns (frames, peaks)."""
+    average as the knee source).  Returns (frames, peaks); knees (a list, if
+    given) receives each frame's (peak, average PQ) -- the static parameters
+    a per-frame check of that frame needs (tests/lp_gate.py)."""
     state = state or PeakState(params)
     static_peak = resolved(params)[0]
     fmax, favg = peak_stats(params, buf, width, height)
@@ -347,6 +357,8 @@ def process_dynamic(params: Params, lattice: 'np.ndarray | None', buf: np.ndarra
         q.peak = pk
         outs.append(process(q, lattice, np.ascontiguousarray(buf[f:f + 1]), width, height, avg_pq=state.avg))
         peaks.append(pk)
+        if knees is not None:
+            knees.append((pk, state.avg))
     return np.concatenate(outs), peaks
 
 

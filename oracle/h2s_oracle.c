@@ -1269,12 +1269,14 @@ int oracle_process(const h2s_params *p, const float *lut, int lut_n, const h2s_f
   return oracle_process_knee(p, lut, lut_n, in, out, nframes, nthreads, 0.0);
 }
 
-/* float RGB (planar) of frame 0 after `stage` */
-int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, int stage,
-                       float *out_rgb) {
+/* float RGB (planar) of frame 0 after `stage`; avg_pq > 0: the spline
+ * knee's source level (peak detection), as oracle_process_knee */
+int oracle_debug_float_knee(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, int stage,
+                            double avg_pq, float *out_rgb) {
   ocfg c;
   int rc = resolve(&c, p, lut, lut_n);
   if (rc) return rc;
+  if (avg_pq > 0.0) spline_setup(&c, avg_pq);
   int W = in->width, H = in->height, cw = W / 2, ch = H / 2;
   size_t plane = (size_t)W * H;
   const float s = (float)(1 << (c.q_bits - 8));
@@ -1302,14 +1304,21 @@ int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h
   return 0;
 }
 
+int oracle_debug_float(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, int stage,
+                       float *out_rgb) {
+  return oracle_debug_float_knee(p, lut, lut_n, in, stage, 0.0, out_rgb);
+}
+
 /* S2 alone on n given linear R'G'B' triples (planar: in_rgb[c * n + i],
  * units of npl, as stage 1 reports them): the tone map the chain applies.
  * Test infrastructure for the float gate's error propagation
  * (tests/float_gate.py: the stage-2 Jacobian by central differences). */
-int oracle_tonemap_lin(const h2s_params *p, const float *lut, int lut_n, const float *in_rgb, int n, float *out_rgb) {
+int oracle_tonemap_lin_knee(const h2s_params *p, const float *lut, int lut_n, const float *in_rgb, int n,
+                            double avg_pq, float *out_rgb) {
   ocfg c;
   int rc = resolve(&c, p, lut, lut_n);
   if (rc) return rc;
+  if (avg_pq > 0.0) spline_setup(&c, avg_pq);
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
@@ -1326,6 +1335,10 @@ int oracle_tonemap_lin(const h2s_params *p, const float *lut, int lut_n, const f
     out_rgb[2 * n + i] = o.b;
   }
   return 0;
+}
+
+int oracle_tonemap_lin(const h2s_params *p, const float *lut, int lut_n, const float *in_rgb, int n, float *out_rgb) {
+  return oracle_tonemap_lin_knee(p, lut, lut_n, in_rgb, n, 0.0, out_rgb);
 }
 
 /* resolved constants, for tests of the parameter logic; returns the
@@ -1366,10 +1379,12 @@ void oracle_set_lp_bias(int codes) { g_lp_bias = codes; }
 /* libplacebo branch with the LUT: the exact pre-rounding value x of each
  * rgba8 download channel of frame 0 (code = floor(x)), planar [3][H][W];
  * H2S_E_UNSUPPORTED on the CPU chain or with the LUT off (no rgba8 download) */
-int oracle_lp_download(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, double *out_x) {
+int oracle_lp_download(const h2s_params *p, const float *lut, int lut_n, const h2s_frames *in, double avg_pq,
+                       double *out_x) {
   ocfg c;
   int rc = resolve(&c, p, lut, lut_n);
   if (rc) return rc;
+  if (avg_pq > 0.0) spline_setup(&c, avg_pq);
   if (c.pipe != H2S_PIPE_LIBPLACEBO || !p->lut_enabled) return H2S_E_UNSUPPORTED;
   const int W = in->width, H = in->height;
   const size_t plane = (size_t)W * H;

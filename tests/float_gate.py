@@ -115,15 +115,15 @@ def tone_uncertainty(params, op):
 class Planes:
     """The oracle's float planes of one frame (stages 1..5, computed on demand)."""
 
-    def __init__(self, params, buf, W, H, lut_n=65):
-        self.params, self.buf, self.W, self.H, self.lut_n = params, buf, W, H, lut_n
+    def __init__(self, params, buf, W, H, lut_n=65, avg_pq=0.0):
+        self.params, self.buf, self.W, self.H, self.lut_n, self.avg_pq = params, buf, W, H, lut_n, avg_pq
         self.op = oracle.params_from(params.to_c())
         self._p = {}
 
     def __getitem__(self, stage):
         if stage not in self._p:
             self._p[stage] = oracle.debug_float(self.op, lattice(self.lut_n), self.buf, self.W, self.H,
-                                                stage).astype(np.float64)
+                                                stage, avg_pq=self.avg_pq).astype(np.float64)
         return self._p[stage]
 
 
@@ -148,8 +148,8 @@ def _stage2_spread(params, P, U1, lin=None):
         hi, lo = lin.copy(), lin.copy()
         hi[k] += h
         lo[k] = np.maximum(lin[k] - h, 0.0)
-        fh = oracle.tonemap_lin(P.op, lat, hi.astype(np.float32)).astype(np.float64)
-        fl = oracle.tonemap_lin(P.op, lat, lo.astype(np.float32)).astype(np.float64)
+        fh = oracle.tonemap_lin(P.op, lat, hi.astype(np.float32), avg_pq=P.avg_pq).astype(np.float64)
+        fl = oracle.tonemap_lin(P.op, lat, lo.astype(np.float32), avg_pq=P.avg_pq).astype(np.float64)
         with np.errstate(invalid='ignore'):
             J = np.nan_to_num((fh - fl) / (hi[k] - lo[k])[None], nan=0.0, posinf=0.0, neginf=0.0)
         out += np.abs(J) * U1[k][None]

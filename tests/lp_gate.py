@@ -86,10 +86,12 @@ def _chroma_any(params, tie, W, H):
     return out
 
 
-def attribute(params, kernel, got, want, src, W, H, lut_n=65, lattice=None):
+def attribute(params, kernel, got, want, src, W, H, lut_n=65, lattice=None, knees=None):
     """Attribute every beyond-one-step sample of got (vs the oracle's want,
     both [F, W*H*3/2] int64) to a download near-tie within the kernel's
-    bound.  src: the input batch (host numpy, [F, ...]).  Returns a report:
+    bound.  src: the input batch (host numpy, [F, ...]).  knees: under
+    dynamic peak detection, each frame's (peak, average PQ) as
+    oracle.process_dynamic(knees=...) reports them.  Returns a report:
     samples, beyond, attributed, unattributed (counts), max_steps, k8_steps,
     near_tie_px (pixels examined that had a channel within the bound)."""
     from float_gate import lattice as _lat
@@ -109,11 +111,15 @@ def attribute(params, kernel, got, want, src, W, H, lut_n=65, lattice=None):
         if not (by[f].any() or bc[f].any()):
             continue
         one = np.ascontiguousarray(src[f:f + 1])
-        P = Planes(params, one, W, H, lut_n)
-        xq = oracle.lp_download(op, lat, one, W, H)               # [3, H, W] exact pre-rounding values
+        pf, avg = params, 0.0
+        if knees is not None:      # this frame's detected peak and knee, as static parameters
+            pf, avg = params.with_(peak=knees[f][0], peak_detect=False), knees[f][1]
+        opf = oracle.params_from(pf.to_c())
+        P = Planes(pf, one, W, H, lut_n, avg_pq=avg)
+        xq = oracle.lp_download(opf, lat, one, W, H, avg_pq=avg)  # [3, H, W] exact pre-rounding values
         need = by[f] | _support(params, bc[f], W, H)
         ys, xs = np.nonzero(need)
-        bound = lp_stage3_bound(params, kernel, P, ys, xs) * qs  # codes
+        bound = lp_stage3_bound(pf, kernel, P, ys, xs) * qs      # codes
         x = xq[:, ys, xs]
         near = (np.abs(x - np.round(x)) <= bound).any(axis=0)
         tie = np.zeros((H, W), bool)
@@ -136,9 +142,9 @@ def attribute(params, kernel, got, want, src, W, H, lut_n=65, lattice=None):
     return rep
 
 
-def check(params, kernel, got, want, src, W, H, lut_n=65, max_attributed_frac=3e-3):
+def check(params, kernel, got, want, src, W, H, lut_n=65, max_attributed_frac=3e-3, knees=None):
     """The gate as failures (empty list = pass)."""
-    rep = attribute(params, kernel, got, want, src, W, H, lut_n)
+    rep = attribute(params, kernel, got, want, src, W, H, lut_n, knees=knees)
     fails = []
     if rep['unattributed']:
         fails.append(f"{rep['unattributed']} samples beyond one step with no download channel within the "

@@ -40,7 +40,7 @@ def test_library_exports_every_symbol():
 def test_abi_version_and_defaults():
     L = _abi.lib()
     assert L.h2s_abi_version() == _abi.ABI_VERSION == 3
-    assert L.h2s_abi_minor() == _abi.ABI_MINOR == 3
+    assert L.h2s_abi_minor() == _abi.ABI_MINOR == 4
     p = _abi.default_params()
     assert (p.transfer_in, p.bits_in, p.bits_out, p.tonemap, p.desat, p.npl, p.gamma, p.lut_enabled) == \
         (0, 10, 10, 6, 2.0, 100.0, 1.0, 1)

@@ -65,4 +65,4 @@ def test_host_pipeline_equals_device_path(tm, case, where):
     assert np.array_equal(got, want)
     if not params.peak_detect:   # (the dynamic peak's oracle flow is tests/test_peak_detect.py's)
         ref = oracle.process(oracle.params_from(params.to_c()), lattice(65), src.to_numpy().buf, W, H).astype(np.int64)
-        assert_close_int(params, want, ref, W, H)
+        assert_close_int(params, want, ref, W, H, src.to_numpy().buf)

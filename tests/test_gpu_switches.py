@@ -191,7 +191,8 @@ def test_libplacebo_tile_equals_generic(tm, case):
     device, same float32 formulas up to the tile kernel's PQ table): the
     bound of assert_close_int with the generic kernel as the reference."""
     params = hdr2sdr.TonemapParams(**LP_CASES[case])
-    src = synth_frames('smooth', 2, 256, 64, params.bits_in, device='cpu', seed=4).to_torch('cuda')
+    host = synth_frames('smooth', 2, 256, 64, params.bits_in, device='cpu', seed=4)
+    src = host.to_torch('cuda')
     tm.set_params(params)
     tm.set_lut(lattice(65))
     tile = tm(src).to_numpy().buf.astype(np.int64)
@@ -200,7 +201,7 @@ def test_libplacebo_tile_equals_generic(tm, case):
         gen = tm(src).to_numpy().buf.astype(np.int64)
     finally:
         tm.set_option(_abi.OPT_FAST_PATH, 1)
-    assert_close_int(params, tile, gen, 256, 64)
+    assert_close_int(params, tile, gen, 256, 64, host.to_numpy().buf)
     assert (tile == gen).mean() > 0.99
 
 
@@ -290,8 +291,9 @@ def test_libplacebo_dynamic_peak(W, H, tmname):
         t.process(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[a:b]), W, H, 10), dst)
         got.append(dst.buf)
     t.close()
-    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
-    assert_close_int(params, np.concatenate(got).astype(np.int64), want.astype(np.int64), W, H)
+    knees = []
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H, knees=knees)
+    assert_close_int(params, np.concatenate(got).astype(np.int64), want.astype(np.int64), W, H, buf, knees=knees)
 
 
 # ---- the reference's second pixel gate --------------------------------------
@@ -396,8 +398,8 @@ def test_rgb48_debug_stage4_matches_oracle(tm):
     assert (d < 1.5 / 65535).mean() > 0.95
 
 
-# H2S_OPT_LP_EXACT (the branch on the generic kernel: the oracle's operation
-# order, glibc's powf / expf, the IPT form in double) over the branch's cases
+# H2S_OPT_LP_EXACT (the branch on the generic kernel: stages 1-3 in exact
+# arithmetic, h2s_lpx.h, as the oracle's chain_lp_d) over the branch's cases
 # without eq (eq after the quantiser spreads a one-step difference) against
 # the oracle: every sample within one output step, on whole tiles and on
 # tiles + tail columns

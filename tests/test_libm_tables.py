@@ -69,3 +69,32 @@ def test_glibc_powf_is_not_the_correctly_rounded_one(libm, tables):
     x, y = f32(0.42890801418277075), f32(1 / PQ_M2)
     cr = f32(float(np.float64(x) ** np.float64(y)))
     assert libm.powf(x, y) == emu_powf(tables, x, y) != cr
+
+
+@pytest.mark.gpu
+def test_device_libm_matches_libm(libm):
+    """ADVICE r05: the device forms themselves (h2s::libm_powf / libm_expf,
+    through the private entry h2stest_libm) equal libm bit for bit on the
+    chain's exponents and random inputs, not only their Python emulation."""
+    import ctypes as C
+    from hdr2sdr import _abi
+    L = C.CDLL(_abi.LIB_PATH)
+    L.h2stest_libm.restype = C.c_int
+    L.h2stest_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(5)
+    ys = [f32(1 / PQ_M2), f32(1 / PQ_M1), PQ_M1, PQ_M2, f32(1 / 2.4), 2.4, 0.2, 1.5]
+    xs = np.concatenate([rng.uniform(0, 1, 3000), rng.uniform(1, 60, 500), 10.0 ** rng.uniform(-44, 0, 500),
+                         [0.0, 1.0, 1e-45, 1.1754944e-38, 0.5, 0.8359375, 1e6, 0.42890801418277075]]).astype(np.float32)
+    for y in ys:
+        yv = np.full(xs.shape, y, np.float32)
+        out = np.empty_like(xs)
+        assert L.h2stest_libm(0, xs.ctypes.data, yv.ctypes.data, out.ctypes.data, xs.size) == 0
+        want = np.array([libm.powf(float(x), y) for x in xs], np.float32)
+        bad = np.nonzero(out.view(np.uint32) != want.view(np.uint32))[0]
+        assert bad.size == 0, [(float(xs[i]), y, float(out[i]), float(want[i])) for i in bad[:5]]
+    ex = np.concatenate([rng.uniform(-0.4, 2.6, 3000), rng.uniform(-104, 89, 1000)]).astype(np.float32)
+    out = np.empty_like(ex)
+    assert L.h2stest_libm(1, ex.ctypes.data, None, out.ctypes.data, ex.size) == 0
+    want = np.array([libm.expf(float(x)) for x in ex], np.float32)
+    bad = np.nonzero(out.view(np.uint32) != want.view(np.uint32))[0]
+    assert bad.size == 0, [(float(ex[i]), float(out[i]), float(want[i])) for i in bad[:5]]

@@ -126,12 +126,13 @@ def test_gpu_dynamic_peak_matches_oracle_across_calls(W, H, tmname, pipeline, mo
     state = tm.peak_state()
     tm.close()
     got = np.concatenate(got).astype(np.int64)
-    want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
+    knees = []
+    want, peaks = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H, knees=knees)
     # the peak really moves (under vf_libplacebo's defaults the darker frames
     # sit at the minimum peak, 1.0 x the 203-nit white)
     assert len(set(round(p, 3) for p in peaks)) >= (3 if model == 'round2' else 2)
     assert state['frames'] == 6 and state['peak'] == pytest.approx(peaks[-1], rel=1e-4)
-    assert_close_int(params, got, want.astype(np.int64), W, H)
+    assert_close_int(params, got, want.astype(np.int64), W, H, buf, knees=knees)
 
 
 @pytest.mark.gpu
@@ -168,8 +169,9 @@ def test_gpu_dynamic_peak_chunked_schedule_is_identical(W, H, pipeline):
         assert runs[chunk][1] == runs[0][1], chunk
         for a, b in zip(runs[chunk][0], runs[0][0]):
             assert np.array_equal(a, b), chunk
-    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
-    assert_close_int(params, runs[4][0][0].astype(np.int64), want.astype(np.int64), W, H)
+    knees = []
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H, knees=knees)
+    assert_close_int(params, runs[4][0][0].astype(np.int64), want.astype(np.int64), W, H, buf, knees=knees)
 
 
 @pytest.mark.gpu
@@ -188,8 +190,9 @@ def test_gpu_dynamic_peak_with_switches_matches_oracle(kw):
     dst = hdr2sdr.FrameBatch.empty_numpy(buf.shape[0], W, H, params.bits_out)
     tm.process(src, dst)
     tm.close()
-    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H)
-    assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H)
+    knees = []
+    want, _ = oracle.process_dynamic(oracle.params_from(params.to_c()), lattice(65), buf, W, H, knees=knees)
+    assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H, buf, knees=knees)
 
 
 @pytest.mark.gpu

@@ -191,8 +191,10 @@ def test_planned_conversion_matches_oracle(tmp_path, cfg):
     dt = np.uint8 if pl.params.bits_out == 8 else np.uint16
     got = np.fromfile(out, dtype=dt).reshape(N, -1).astype(np.int64)
     op = oracle.params_from(pl.params.to_c())
+    knees = None
     if pl.params.peak_detect:      # C3: libplacebo peak_detect=1 -> detected, smoothed peak
-        want = oracle.process_dynamic(op, lattice(65), src.buf, W, H)[0].astype(np.int64)
+        knees = []
+        want = oracle.process_dynamic(op, lattice(65), src.buf, W, H, knees=knees)[0].astype(np.int64)
     else:
         want = oracle.process(op, lattice(65), src.buf, W, H).astype(np.int64)
-    assert_close_int(pl.params, got, want, W, H)
+    assert_close_int(pl.params, got, want, W, H, src.buf, knees=knees)
