@@ -446,6 +446,14 @@ struct HistRun {
     }
     n++;
   }
+  // n values of bin b (a whole quad-form unit in one step)
+  __device__ __forceinline__ void add_n(unsigned* lh, int b, unsigned k) {
+    if (b != bin) {
+      if (n) atomicAdd(&lh[bin], n);
+      bin = b, n = 0;
+    }
+    n += k;
+  }
   __device__ __forceinline__ void flush(unsigned* lh) {
     if (n) atomicAdd(&lh[bin], n);
     n = 0;
@@ -473,50 +481,64 @@ __device__ __forceinline__ void peak_reduce(float mx, float sm, float2* out) {
 }
 
 // ---- dynamic peak: per-frame statistic and curve records on the device ----
-// One frame's (PQ peak measurement, average PQ) from its PEAK_BLOCKS partial
-// (max, sum) records, folded in order (as the oracle's accumulation), and for
-// pd_percentile < 100 the percentile from the frame's histogram: the first
-// bin whose cumulative count reaches pct % of the pixels, interpolated
-// linearly inside it, capped at the frame maximum (oracle_peak_stats).  Counts
-// are integers, so the block scan's u64 sums equal a serial double
-// accumulation exactly.  The histogram is left zeroed for the next call.
-// 256 threads.
+// One frame's (PQ peak measurement, average PQ) from its nblocks partial
+// (max, sum) records and, for pd_percentile < 100, the percentile from the
+// frame's histogram: the first bin whose cumulative count reaches pct % of
+// the pixels, interpolated linearly inside it, capped at the frame maximum
+// (oracle_peak_stats).  Wave-level reductions and scans (no LDS tree): the
+// records fold in a fixed pairwise order in double (deterministic, so sharded
+// and sequential statistics stay bit-identical), the counts are integers (a
+// u32 scan equals a serial accumulation exactly).  The histogram is left
+// zeroed for the next call.  256 threads.
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
 __device__ void peak_frame_fold(const float2* partial, unsigned* hist, const PeakModel& M, double2* fstat, int f) {
-  const int t = threadIdx.x;
-  __shared__ double s_mx, s_sum;
-  __shared__ unsigned long long s_scan[256];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  __shared__ double s_sum[4];
+  __shared__ float s_mx[4];
+  __shared__ unsigned s_wtot[4];
   __shared__ int s_bin;
-  __shared__ float2 s_part[PEAK_BLOCKS_MAX];
   static_assert(PEAK_BLOCKS_MAX <= 256, "one partial record per thread");
-  if (t < M.nblocks) s_part[t] = partial[(size_t)f * M.nblocks + t];   // all loads in flight at once
-  __syncthreads();
-  if (t == 0) {
-    double mx = 0.0, sum = 0.0;
-    for (int b = 0; b < M.nblocks; b++) {
-      const float2 v = s_part[b];
-      mx = v.x > mx ? v.x : mx;
-      sum += v.y;
-    }
-    s_mx = mx, s_sum = sum;
-    s_bin = PEAK_BINS;
-  }
+  const float2 rec = t < M.nblocks ? partial[(size_t)f * M.nblocks + t] : make_float2(0.0f, 0.0f);
+  const double ws = wave_sum_d((double)rec.y);
+  const float wm = wave_max_f(rec.x);
+  if (lane == 0) s_sum[w] = ws, s_mx[w] = wm;
+  if (t == 0) s_bin = PEAK_BINS;
+  unsigned cnt[4] = {0u, 0u, 0u, 0u}, incl = 0u;
   if (M.pct) {
     static_assert(PEAK_BINS == 4 * 256, "four bins per thread");
     uint4* h = reinterpret_cast<uint4*>(hist + (size_t)f * PEAK_BINS);
     const uint4 c = h[t];
     h[t] = make_uint4(0u, 0u, 0u, 0u);
-    const unsigned cnt[4] = {c.x, c.y, c.z, c.w};
-    s_scan[t] = (unsigned long long)c.x + c.y + c.z + c.w;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {   // inclusive Hillis-Steele scan
-      const unsigned long long add = t >= o ? s_scan[t - o] : 0ull;
-      __syncthreads();
-      s_scan[t] += add;
-      __syncthreads();
+    cnt[0] = c.x, cnt[1] = c.y, cnt[2] = c.z, cnt[3] = c.w;
+    incl = c.x + c.y + c.z + c.w;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {   // inclusive scan within the wave
+      const unsigned v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
     }
-    const double n = (double)s_scan[255];
-    const double target = M.percentile / 100.0 * n;
-    double cum = (double)(s_scan[t] - ((unsigned long long)c.x + c.y + c.z + c.w));
+    if (lane == 63) s_wtot[w] = incl;
+  }
+  __syncthreads();
+  const double sum = (s_sum[0] + s_sum[1]) + (s_sum[2] + s_sum[3]);
+  const double mx = (double)fmaxf(fmaxf(s_mx[0], s_mx[1]), fmaxf(s_mx[2], s_mx[3]));
+  if (M.pct) {
+    unsigned before = 0u, n = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      before += k < w ? s_wtot[k] : 0u;
+      n += s_wtot[k];
+    }
+    const double target = M.percentile / 100.0 * (double)n;
+    double cum = (double)(before + incl - (cnt[0] + cnt[1] + cnt[2] + cnt[3]));
     int mine = PEAK_BINS;
     double cum_at = 0.0;
     for (int k = 0; k < 4; k++) {
@@ -527,37 +549,51 @@ __device__ void peak_frame_fold(const float2* partial, unsigned* hist, const Pea
     __syncthreads();
     if (mine < PEAK_BINS && mine == s_bin) {   // the owner of the first bin
       const double v = (mine + (target - cum_at) / cnt[mine & 3]) / PEAK_BINS;
-      fstat[f] = make_double2(v < s_mx ? v : s_mx, s_sum / M.npx);
+      fstat[f] = make_double2(v < mx ? v : mx, sum / M.npx);
     } else if (t == 0 && s_bin == PEAK_BINS) {
-      fstat[f] = make_double2(s_mx, s_sum / M.npx);
+      fstat[f] = make_double2(mx, sum / M.npx);
     }
-  } else {
-    __syncthreads();
-    if (t == 0) fstat[f] = make_double2(s_mx, s_sum / M.npx);
+  } else if (t == 0) {
+    fstat[f] = make_double2(mx, sum / M.npx);
   }
 }
 
 // The IIR over n frames in order (thread 0, from the state the previous calls
 // left in *st), then each frame's peak and curve record in parallel.
-// out = null: the state only.  Every thread of the block calls it.
+// out = null: the state only.  Every thread of the block calls it.  The
+// frames' statistics are staged through LDS, PEAK_IIR_CHUNK at a time, so
+// the serial recurrence reads LDS instead of making a global round trip per
+// frame (its loads could not be hoisted past the stores of the smoothed
+// values: finish 20.8 -> see DESIGN.md §4.6)
+constexpr int PEAK_IIR_CHUNK = 1024;
 __device__ void peak_curves_body(double2* fstat, int n, const PeakModel& M, PeakState* st, CurveConsts* out) {
   const int t = threadIdx.x;
-  if (t == 0) {
-    PeakState s = *st;
-    for (int f = 0; f < n; f++) {
-      const double2 v = fstat[f];
-      peak_iir_step(&s, M, v.x, v.y);
-      fstat[f] = make_double2(s.max, s.avg);   // the smoothed values frame f's curve uses
+  __shared__ double2 s_f[PEAK_IIR_CHUNK];
+  __shared__ PeakState s_st;
+  if (t == 0) s_st = *st;
+  for (int c0 = 0; c0 < n; c0 += PEAK_IIR_CHUNK) {
+    const int cn = n - c0 < PEAK_IIR_CHUNK ? n - c0 : PEAK_IIR_CHUNK;
+    __syncthreads();
+    for (int f = t; f < cn; f += blockDim.x) s_f[f] = fstat[c0 + f];
+    __syncthreads();
+    if (t == 0) {
+      PeakState s = s_st;
+      for (int f = 0; f < cn; f++) {
+        peak_iir_step(&s, M, s_f[f].x, s_f[f].y);
+        s_f[f] = make_double2(s.max, s.avg);   // the smoothed values frame f's curve uses
+      }
+      s_st = s;
     }
-    if (n > 0) s.peak = peak_of(M, s.max);
-    *st = s;
+    __syncthreads();
+    for (int f = t; f < cn; f += blockDim.x) {
+      fstat[c0 + f] = s_f[f];
+      const double pk = peak_of(M, s_f[f].x);
+      if (c0 + f == n - 1) s_st.peak = pk;    // the state's peak: the last frame's (its smoothed max)
+      if (out) curve_for_peak(M, pk, s_f[f].y, &out[c0 + f]);
+    }
   }
   __syncthreads();
-  if (!out) return;
-  for (int f = t; f < n; f += blockDim.x) {
-    const double2 v = fstat[f];
-    curve_for_peak(M, peak_of(M, v.x), v.y, &out[f]);
-  }
+  if (t == 0) *st = s_st;
 }
 
 // k_peak_finish: one block per frame folds that frame's records (and clears
@@ -614,17 +650,13 @@ __global__ __launch_bounds__(256) void k_peak_stats(const KParams P, float2* par
 
 // streaming form (W % 8 == 0, 16-byte luma / 8-byte chroma alignment): each
 // thread takes 8-pixel row chunks (one 16-byte luma load, one 8-byte load per
-// chroma plane), two chunks per iteration so two loads per plane are in flight.
-// ROW2 (A/B, H2S_OPT_TEST_PEAK_FORM 1; PQ input): a 2 x 8 luma chunk with its 4
-// chroma samples (one chroma row feeds two luma rows), the chroma terms
-// maximised once per sample (max(Y + dr, Y + dg, Y + db) == Y + max(dr, dg, db):
-// rounding is monotonic).  Fewer loads and VALU per pixel, yet measured 165 us
-// against 104 us for 16 4K frames (round 5, profiles/r05/peak_ab): the default
-// stays the row form
+// chroma plane), four chunks' loads in flight.  The round-5 default; the A/B
+// reference of the quad form below (H2S_OPT_TEST_PEAK_FORM 1) and the form
+// for HLG input
 #ifndef H2S_PEAK_INFLIGHT
 #define H2S_PEAK_INFLIGHT 4
 #endif
-template <int TRC, bool HIST, bool ROW2 = false>
+template <int TRC, bool HIST>
 __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* partial, const PeakTail T) {
   __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *T.done = 0u;   // k_peak_finish's counter (stream-ordered)
@@ -633,75 +665,37 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
   if (HIST) __syncthreads();
   const int f = blockIdx.y;
   const int cpr = P.W >> 3;                       // chunks per row
-  const int rows = ROW2 ? (P.H + 1) >> 1 : P.H;   // chunk rows: luma row pairs (PQ) or rows
-  const int nch = rows * cpr, stride = gridDim.x * 256;
+  const int nch = P.H * cpr, stride = gridDim.x * 256;
   const uint8_t* y0 = P.in[0] + f * P.in_fp[0];
   const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
   const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
-  const unsigned m2 = P.in_mask | (P.in_mask << 16);
   float mx = 0.0f, sm = 0.0f;
   HistRun run;
   struct Chunk {
-    uint4 ya, yb;
+    uint4 ya;
     uint2 ua, va;
-    bool two;
   };
   auto load = [&](int i, Chunk& c) {
     const int r = i / cpr, cx = i - r * cpr;
-    if (ROW2) {
-      const int y = 2 * r;
-      c.two = y + 1 < P.H;
-      c.ya = reinterpret_cast<const uint4*>(y0 + y * P.in_ls[0])[cx];
-      c.yb = c.two ? reinterpret_cast<const uint4*>(y0 + (y + 1) * P.in_ls[0])[cx] : c.ya;
-      c.ua = reinterpret_cast<const uint2*>(u0 + r * P.in_ls[1])[cx];
-      c.va = reinterpret_cast<const uint2*>(v0 + r * P.in_ls[2])[cx];
-    } else {
-      c.two = false;
-      c.ya = reinterpret_cast<const uint4*>(y0 + r * P.in_ls[0])[cx];
-      c.ua = reinterpret_cast<const uint2*>(u0 + (r >> 1) * P.in_ls[1])[cx];
-      c.va = reinterpret_cast<const uint2*>(v0 + (r >> 1) * P.in_ls[2])[cx];
-    }
+    c.ya = reinterpret_cast<const uint4*>(y0 + r * P.in_ls[0])[cx];
+    c.ua = reinterpret_cast<const uint2*>(u0 + (r >> 1) * P.in_ls[1])[cx];
+    c.va = reinterpret_cast<const uint2*>(v0 + (r >> 1) * P.in_ls[2])[cx];
   };
   auto fold = [&](const Chunk& c) {
     const unsigned uu[4] = {c.ua.x & 0xffff, c.ua.x >> 16, c.ua.y & 0xffff, c.ua.y >> 16};
     const unsigned vv[4] = {c.va.x & 0xffff, c.va.x >> 16, c.va.y & 0xffff, c.va.y >> 16};
+    const unsigned yy[8] = {c.ya.x & 0xffff, c.ya.x >> 16, c.ya.y & 0xffff, c.ya.y >> 16,
+                            c.ya.z & 0xffff, c.ya.z >> 16, c.ya.w & 0xffff, c.ya.w >> 16};
     float rs = 0.0f;
-    if (ROW2) {
-      float d[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const float cb = (float)(uu[k] & P.in_mask) * P.c_scale + P.c_off;
-        const float cr = (float)(vv[k] & P.in_mask) * P.c_scale + P.c_off;
-        d[k] = fmaxf(fmaxf(P.m_rcr * cr, P.m_gcb * cb + P.m_gcr * cr), P.m_bcb * cb);
-      }
-      auto row = [&](const uint4 ya) {
-        const unsigned w[4] = {ya.x & m2, ya.y & m2, ya.z & m2, ya.w & m2};
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const unsigned code = (k & 1) ? w[k >> 1] >> 16 : w[k >> 1] & 0xffff;
-          const float m = clamp01((float)code * P.y_scale + P.y_off + d[k >> 1]);
-          mx = fmaxf(mx, m);
-          rs += m;
-          if (HIST) run.add(lh, m);
-        }
-      };
-      row(c.ya);
-      if (c.two) row(c.yb);
-    } else {
-      const unsigned yy[8] = {c.ya.x & 0xffff, c.ya.x >> 16, c.ya.y & 0xffff, c.ya.y >> 16,
-                              c.ya.z & 0xffff, c.ya.z >> 16, c.ya.w & 0xffff, c.ya.w >> 16};
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
-        mx = fmaxf(mx, m);
-        rs += m;
-        if (HIST) run.add(lh, m);
-      }
+    for (int k = 0; k < 8; k++) {
+      const float m = peak_px<TRC>(P, yy[k], uu[k >> 1], vv[k >> 1]);
+      mx = fmaxf(mx, m);
+      rs += m;
+      if (HIST) run.add(lh, m);
     }
     sm += rs;
   };
-  // H2S_PEAK_INFLIGHT chunks' loads issued before the first is folded (the
-  // kernel is latency-bound: one block-wave of 64 blocks per frame)
   int i = blockIdx.x * 256 + threadIdx.x;
   for (; i + (H2S_PEAK_INFLIGHT - 1) * stride < nch; i += H2S_PEAK_INFLIGHT * stride) {
     Chunk c[H2S_PEAK_INFLIGHT];
@@ -720,6 +714,104 @@ __global__ __launch_bounds__(256) void k_peak_stats_v(const KParams P, float2* p
   peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
 }
 
+// quad form, the default for PQ input (W % 16 == 0, 16-byte rows; VERDICT
+// r05 item 4): a thread's unit is 32 pixels -- 16 columns of a luma row pair
+// and their 8 chroma samples -- read as six 16-byte loads (no chroma row read
+// twice), two units' loads in flight.  PQ(max EOTF(R'G'B')) = clamp(max E):
+// the chroma terms are maximised once per chroma sample (with Y's offset:
+// d = y_off + max(a_rv v, a_gu u + a_gv v, a_bu u)) and each pixel is one FMA
+// clamped to [0, 1] (E = code ys + d).  The histogram (pd_percentile < 100)
+// takes a whole unit in one run step when the unit's smallest and largest
+// values share a bin (bin() is monotonic), which is nearly every unit on real
+// content; units that span bins add per pixel.  Every sum runs in a fixed
+// order within the frame (unit by unit, 32 pixels row by row), so sharded
+// and sequential statistics stay bit-identical.
+template <bool HIST, int INF = 2>   // INF: units whose loads are in flight (4: A/B, H2S_OPT_TEST_PEAK_FORM 2)
+__global__ __launch_bounds__(256) void k_peak_stats_q(const KParams P, float2* partial, const PeakTail T) {
+  __shared__ unsigned lh[HIST ? PEAK_BINS : 1];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *T.done = 0u;   // k_peak_finish's counter (stream-ordered)
+  if (HIST)
+    for (int i = threadIdx.x; i < PEAK_BINS; i += 256) lh[i] = 0;
+  if (HIST) __syncthreads();
+  const int f = blockIdx.y;
+  const int cpr = P.W >> 4, nch = (P.H >> 1) * cpr, stride = gridDim.x * 256;
+  const uint8_t* y0 = P.in[0] + f * P.in_fp[0];
+  const uint8_t* u0 = P.in[1] + f * P.in_fp[1];
+  const uint8_t* v0 = P.in[2] + f * P.in_fp[2];
+  const unsigned m2 = P.in_mask | (P.in_mask << 16);
+  const float ys = P.y_scale, yo = P.y_off, cs = P.c_scale, co = P.c_off;
+  float mx = 0.0f, sm = 0.0f;
+  HistRun run;
+  struct Unit {
+    uint4 u, v, y0a, y0b, y1a, y1b;
+  };
+  auto load = [&](int i, Unit& q) {
+    const int r = i / cpr, cx = i - r * cpr;
+    q.u = *reinterpret_cast<const uint4*>(u0 + r * P.in_ls[1] + 16 * cx);
+    q.v = *reinterpret_cast<const uint4*>(v0 + r * P.in_ls[2] + 16 * cx);
+    const uint4* ya = reinterpret_cast<const uint4*>(y0 + 2 * r * P.in_ls[0] + 32 * cx);
+    const uint4* yb = reinterpret_cast<const uint4*>(y0 + (2 * r + 1) * P.in_ls[0] + 32 * cx);
+    q.y0a = ya[0], q.y0b = ya[1], q.y1a = yb[0], q.y1b = yb[1];
+  };
+  // the 32 values of a unit, in order, to fn(m)
+  auto each = [&](const Unit& q, const float (&d)[8], auto&& fn) {
+    const uint4 rows[4] = {q.y0a, q.y0b, q.y1a, q.y1b};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      const unsigned w[4] = {rows[h].x & m2, rows[h].y & m2, rows[h].z & m2, rows[h].w & m2};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const unsigned code = (k & 1) ? w[k >> 1] >> 16 : w[k >> 1] & 0xffffu;
+        fn(__builtin_amdgcn_fmed3f(fmaf((float)code, ys, d[4 * (h & 1) + (k >> 1)]), 0.0f, 1.0f));
+      }
+    }
+  };
+  auto fold = [&](const Unit& q) {
+    const unsigned ua[4] = {q.u.x & m2, q.u.y & m2, q.u.z & m2, q.u.w & m2};
+    const unsigned va[4] = {q.v.x & m2, q.v.y & m2, q.v.z & m2, q.v.w & m2};
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const float cb = fmaf((float)((j & 1) ? ua[j >> 1] >> 16 : ua[j >> 1] & 0xffffu), cs, co);
+      const float cr = fmaf((float)((j & 1) ? va[j >> 1] >> 16 : va[j >> 1] & 0xffffu), cs, co);
+      d[j] = yo + fmaxf(fmaxf(P.m_rcr * cr, fmaf(P.m_gcb, cb, P.m_gcr * cr)), P.m_bcb * cb);
+    }
+    float rs = 0.0f, umx = 0.0f, umn = 1.0f;
+    each(q, d, [&](float m) {
+      umx = fmaxf(umx, m);
+      umn = fminf(umn, m);
+      rs += m;
+    });
+    mx = fmaxf(mx, umx);
+    sm += rs;
+    if (HIST) {
+      const int b0 = min((int)(umn * (float)PEAK_BINS), PEAK_BINS - 1);
+      const int b1 = min((int)(umx * (float)PEAK_BINS), PEAK_BINS - 1);
+      if (b0 == b1) {
+        run.add_n(lh, b0, 32u);
+      } else {
+        each(q, d, [&](float m) { run.add(lh, m); });
+      }
+    }
+  };
+  int i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + (INF - 1) * stride < nch; i += INF * stride) {
+    Unit q[INF];
+#pragma unroll
+    for (int k = 0; k < INF; k++) load(i + k * stride, q[k]);
+#pragma unroll
+    for (int k = 0; k < INF; k++) fold(q[k]);
+  }
+  for (; i < nch; i += stride) {
+    Unit q;
+    load(i, q);
+    fold(q);
+  }
+  if (HIST) run.flush(lh);
+  if (HIST) hist_flush(lh, T.hist + (size_t)f * PEAK_BINS);
+  peak_reduce(mx, sm, &partial[f * gridDim.x + blockIdx.x]);
+}
+
 // the statistics of P's frames, then (k_peak_finish) their (measurement,
 // average) in T.fstat and, T.st set, the smoothed state and curve records:
 // two launches
@@ -727,15 +819,20 @@ hipError_t launch_peak_stats(const KParams& P, float2* partial, const PeakTail& 
   if (P.nframes <= 0) return hipSuccess;
   const dim3 grid(T.M.nblocks, P.nframes);
   auto al = [](long long v, int a) { return (v & (a - 1)) == 0; };
-  const bool vec = P.W % 8 == 0 && al((long long)(uintptr_t)P.in[0], 16) && al(P.in_ls[0], 16) &&
-                   al(P.in_fp[0], 16) && al((long long)(uintptr_t)P.in[1], 8) && al(P.in_ls[1], 8) &&
-                   al(P.in_fp[1], 8) && al((long long)(uintptr_t)P.in[2], 8) && al(P.in_ls[2], 8) &&
-                   al(P.in_fp[2], 8);
+  auto planes_al = [&](int ya, int ca) {
+    return al((long long)(uintptr_t)P.in[0], ya) && al(P.in_ls[0], ya) && al(P.in_fp[0], ya) &&
+           al((long long)(uintptr_t)P.in[1], ca) && al(P.in_ls[1], ca) && al(P.in_fp[1], ca) &&
+           al((long long)(uintptr_t)P.in[2], ca) && al(P.in_ls[2], ca) && al(P.in_fp[2], ca);
+  };
+  const bool vec = P.W % 8 == 0 && planes_al(16, 8);
+  const bool quad = P.W % 16 == 0 && P.transfer == 0 && T.form != 1 && planes_al(16, 16);
 #define H2S_PEAK_LAUNCH(HI)                                                                   \
-  if (vec && P.transfer == 1)                                                                 \
+  if (quad && T.form == 2)                                                                    \
+    hipLaunchKernelGGL((k_peak_stats_q<HI, 4>), grid, dim3(256), 0, s, P, partial, T);        \
+  else if (quad)                                                                              \
+    hipLaunchKernelGGL((k_peak_stats_q<HI>), grid, dim3(256), 0, s, P, partial, T);           \
+  else if (vec && P.transfer == 1)                                                            \
     hipLaunchKernelGGL((k_peak_stats_v<1, HI>), grid, dim3(256), 0, s, P, partial, T);        \
-  else if (vec && T.form == 1)                                                                \
-    hipLaunchKernelGGL((k_peak_stats_v<0, HI, true>), grid, dim3(256), 0, s, P, partial, T);  \
   else if (vec)                                                                               \
     hipLaunchKernelGGL((k_peak_stats_v<0, HI>), grid, dim3(256), 0, s, P, partial, T);        \
   else if (P.transfer == 1)                                                                   \

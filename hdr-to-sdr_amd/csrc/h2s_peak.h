@@ -20,7 +20,7 @@
 
 namespace h2s {
 
-constexpr int PEAK_BLOCKS = 64;       // partial (max, sum) records per frame (k_peak_stats*), default
+constexpr int PEAK_BLOCKS = 128;      // partial (max, sum) records per frame (k_peak_stats*), default (round 6: 64 -> 128)
 constexpr int PEAK_BLOCKS_MAX = 256;  // ... at most (H2S_OPT_TEST_PEAK_BLOCKS A/B; one per finish thread)
 constexpr int PEAK_BINS = 1024;  // percentile histogram bins over PQ [0, 1]
 
@@ -64,7 +64,7 @@ struct PeakTail {
   PeakState* st;       // null: the statistics only (h2s_peak_stats)
   CurveConsts* out;    // nframes curve records, or null
   int nframes;
-  int form;            // PQ streaming form: 0 = 8-pixel row chunks, 1 = 2 x 8 chunks (test hook A/B)
+  int form;            // PQ statistics form: 0 = 32-pixel quad units (default), 1 = 8-pixel row chunks (test hook A/B)
 };
 
 __host__ __device__ inline double hd_pq_encode(double y) {

@@ -225,7 +225,7 @@ enum h2s_option {
 /* 1 = the next h2s_process call reports H2S_E_HIP right after queueing its
  * kernels (the error exits must still record the launch) */
 #define H2S_OPT_TEST_FAIL_AFTER_LAUNCH (H2S_OPT_PRIVATE_BASE + 1)
-/* peak statistics kernel form (A/B measurements): 0 = row chunks (default), 1 = 2 x 8 chunks */
+/* peak statistics kernel form (A/B measurements): 0 = 32-pixel quad units (default), 1 = round 5's row chunks */
 #define H2S_OPT_TEST_PEAK_FORM (H2S_OPT_PRIVATE_BASE + 2)
 /* dynamic peak on the tile kernel: frames per pipelined chunk (0 = statistics for
  * the whole batch, then one conversion launch) */

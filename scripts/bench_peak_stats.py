@@ -41,12 +41,27 @@ for dyn in (False, True):
     p = hdr2sdr.TonemapParams(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=dyn, maxcll=4000.0)
     tm = hdr2sdr.Tonemapper(0, p, lat)
     out = tm(src)            # allocates a device batch of the right shape
-    forms = (0, 1) if dyn else (0,)
+    forms = (0, 1, 2) if dyn else (0,)   # 0: quad units (default), 1: round-5 row chunks, 2: quad, 4 in flight
     for form in forms:
         tm.set_option(_abi.OPT_TEST_PEAK_FORM, form)
         res[f'{"dyn" if dyn else "static"}_form{form}_ms'] = round(timed(tm, out), 4)
         print(json.dumps(res), flush=True)
+    if dyn:   # partial records (blocks) per frame, quad form
+        tm.set_option(_abi.OPT_TEST_PEAK_FORM, 0)
+        for nb in (128, 256, 64):
+            tm.set_option(_abi.OPT_TEST_PEAK_BLOCKS, nb)
+            res[f'dyn_form0_blocks{nb}_ms'] = round(timed(tm, out), 4)
+            print(json.dumps(res), flush=True)
+    tm.close()
+# the statistics alone (h2s_peak_stats: the finish kernel without IIR / curve
+# records), and without the histogram (pd_percentile 100), for the trace
+for pct in (float('nan'), 100.0):
+    p = hdr2sdr.TonemapParams(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=True, maxcll=4000.0,
+                              pd_percentile=pct)
+    tm = hdr2sdr.Tonemapper(0, p, lat)
+    for _ in range(20):
+        tm.peak_stats(src)
     tm.close()
 res['dyn_minus_static_form0'] = round(res['dyn_form0_ms'] - res['static_form0_ms'], 4)
-res['dyn_minus_static_form1'] = round(res['dyn_form1_ms'] - res['static_form0_ms'], 4)
+res['dyn_minus_static_form1'] = round(res['dyn_form1_ms'] - res['static_form0_ms'], 4)  # round 5's row form
 print(json.dumps(res))
