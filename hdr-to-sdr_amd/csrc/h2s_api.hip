@@ -939,7 +939,6 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->log2_nm1 = (float)log2((double)(n - 1));
   F->s_max = nextafterf((float)(n - 1), 0.0f);
   F->x_max = 0.999999f;  // (N-1) * x_max^(1/2.4) stays > 3 ulp below N-1
-  F->stride_r = 12.0f;
   F->stride_g = (float)(12 * n);
   F->stride_b = (float)(12 * n * n);
   F->og = 12 * n;

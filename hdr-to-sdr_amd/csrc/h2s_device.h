@@ -197,7 +197,6 @@ struct FastParams : CurveConsts {
                                    // the base CurveConsts is the batch's curve)
   // S3/S4: lattice coordinates and byte offsets (float4 records)
   float log2_nm1, s_max, stride_g, stride_b;  // byte strides 12N, 12N^2 (as floats)
-  float stride_r;                              // 12 (the cell-major A/B layout: 128)
   float x_max;                                 // largest x with (N-1) x^(1/2.4) < N-1 (margin)
   int og, ob, cr, cg, cb, c111;                // corner byte offsets
   const float* lut_yuv;                        // 12-byte records (Y', Cb', Cr')

@@ -43,52 +43,11 @@ __global__ void k_build_lut_yuv(const float4* rgb, float* yuv, int n3, const Yuv
 
 bool fast_supported(int tonemap) { return tonemap >= 4 && tonemap <= 8; }
 
-#if H2S_CELL_LAYOUT
-// A/B build only (the brick-layout candidate in its
-// zero-address-cost form): the lattice stored cell-major, each cell's eight
-// corner records (corner a + 2b + 4c at 12 (a + 2b + 4c) bytes) in one
-// 128-byte line, corners past the lattice edge clamped.  Every tetrahedron's
-// four records then sit in one line, and the kernel's addressing is unchanged
-// but for the strides (128, 128 N, 128 N^2 instead of 12, 12 N, 12 N^2).  The
-// N^3 x 128 B lattice (35 MB at N = 65) lives in a buffer of this TU's own,
-// filled from the linear one after every build (one lattice per process: an
-// ablation build, not the product).
-static float* g_cell = nullptr;
-static int g_cell_n = 0;
-
-__global__ void k_build_lut_cell(const float* lin, float* cell, int n) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= n * n * n) return;
-  const int i = c % n, j = (c / n) % n, k = c / (n * n);
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const int a = min(i + (q & 1), n - 1), b = min(j + ((q >> 1) & 1), n - 1), d = min(k + (q >> 2), n - 1);
-    const float* r = lin + 3 * ((long long)(d * n + b) * n + a);
-    float* o = cell + 32 * (long long)c + 3 * q;
-    o[0] = r[0], o[1] = r[1], o[2] = r[2];
-  }
-}
-#endif
-
 // desat: 0 off, 1 weighted luma, 2 RGB-coefficient luma (vf_tonemap's; the
 // libplacebo curves have none).  lp: the libplacebo branch (every operator).
 // dbg: 0 = the
 // product kernel; 1..5 = its debug instance for that h2s_stage (F.dbg set)
-hipError_t launch_fast(const FastParams& F0, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
-#if H2S_CELL_LAYOUT
-  FastParams F = F0;
-  if (F.lut_yuv && g_cell) {
-    const int n = g_cell_n;
-    F.lut_yuv = g_cell;
-    F.lut_bytes = 128 * n * n * n;
-    F.stride_r = 128.0f;
-    F.stride_g = (float)(128 * n);
-    F.stride_b = (float)(128 * n * n);
-    F.og = 24, F.ob = 48, F.c111 = 84, F.cr = 72, F.cg = 60, F.cb = 36;
-  }
-#else
-  const FastParams& F = F0;
-#endif
+hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, hipStream_t s, int dbg) {
   const long long nt = (long long)F.nbx * F.nby * F.nframes;
   if (nt == 0) return hipSuccess;
   const long long nb = (nt + F.tpb - 1) / F.tpb;
@@ -114,15 +73,6 @@ hipError_t launch_fast(const FastParams& F0, int trc, int tm, int desat, int lp,
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st) {
   const int n3 = n * n * n;
   hipLaunchKernelGGL(k_build_lut_yuv, dim3((n3 + 255) / 256), dim3(256), 0, st, rgb, yuv, n3, K);
-#if H2S_CELL_LAYOUT
-  if (g_cell_n != n) {
-    if (g_cell) hipFree(g_cell);
-    g_cell = nullptr;
-    if (hipMalloc((void**)&g_cell, (size_t)n3 * 128) != hipSuccess) return hipErrorOutOfMemory;
-    g_cell_n = n;
-  }
-  hipLaunchKernelGGL(k_build_lut_cell, dim3((n3 + 255) / 256), dim3(256), 0, st, yuv, g_cell, n);
-#endif
   return hipGetLastError();
 }
 

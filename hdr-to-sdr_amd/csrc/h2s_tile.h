@@ -35,7 +35,7 @@
 // switchable for A/B builds, scripts/build_variants.sh):
 //  H2S_TAGSEL    tetrahedron from axis-tagged fractions + a 3-entry LDS
 //                offset table, one-key uniformity test (9 + 6 half-rate ops -> 6)
-//  H2S_EXPCLAMP  lut3d's [0, N-1] clamp as v_exp_f32's output clamp
+//  (EXPCLAMP)    lut3d's [0, N-1] clamp as v_exp_f32's output clamp
 //  H2S_EQMAGIC   eq index by a 2^23 add and a 16-bit shift (full-rate ops)
 // The PQ table's first segment (E' < 1/128, below ~0.0015 nits), where the
 // EOTF ~ (E - E0)^6.28 and no cubic holds 1e-3 relative, is staged as the
@@ -47,9 +47,6 @@
 #ifndef H2S_TAGSEL
 #define H2S_TAGSEL 1
 #endif
-#ifndef H2S_EXPCLAMP
-#define H2S_EXPCLAMP 1
-#endif
 #ifndef H2S_EQMAGIC
 #define H2S_EQMAGIC 1
 #endif
@@ -57,21 +54,6 @@
 namespace h2s {
 
 typedef float f3 __attribute__((ext_vector_type(3)));
-#ifndef H2S_CELL_LAYOUT
-#define H2S_CELL_LAYOUT 0   // 1: the cell-major lattice A/B (h2s_fast.hip): the r stride from FastParams
-#endif
-#ifndef H2S_LDS_BOX
-#define H2S_LDS_BOX 0   // 1: the LDS-staged lattice box on the CPU chain (A/B, px_chain)
-#endif
-#ifndef H2S_PATCH_WALK
-#define H2S_PATCH_WALK 0   // 1: a block's 8 tiles as a 4 x 2 patch (A/B, tile_geo_patch)
-#endif
-#ifndef H2S_LP_LUT8TAB
-#define H2S_LP_LUT8TAB 1   // libplacebo lut3d 8-bit coordinates from the block's (cell, fraction) table; 0: per pixel (A/B)
-#endif
-#ifndef H2S_LP_BLEND_FUSED
-#define H2S_LP_BLEND_FUSED 0   // 1: the libplacebo blend contracted into FMAs (pre-round-5 code, A/B)
-#endif
 
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
@@ -434,15 +416,12 @@ __device__ __forceinline__ float lut_s(const FastParams& F, float x) {
 struct StepK {
   float a_rv, a_gv, a_gu, a_bu;   // chroma terms of E, x ESC
   float stride_g, stride_b;       // lattice byte strides (as floats)
-  float stride_r;
   int og, ob, ocr, ocg, ocb;      // corner byte offsets
   float log2_nm1, x_max;
   float hable_kb;                 // F.hable_kb (Hable instances)
   int c111;                       // the far corner's byte offset
   float nm1;                      // N - 1
   const int* offtab;              // LDS: byte offset of the +1 corner along r, g, b at bytes 0, 4, 8
-  float* box;                     // H2S_LDS_BOX: this wave's 4 x 4 x 4-node box (64 x 3 floats)
-  int boxofs;                     // ... byte offset of this lane's box node from the anchor cell's origin
 };
 
 // One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
@@ -544,24 +523,12 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
         };
         dput(ev(r), ev(gg), ev(bl));
       }
-#if H2S_LP_LUT8TAB
       const float2 tr = lut8_lds[q8(r)], tg = lut8_lds[q8(gg)], tb = lut8_lds[q8(bl)];
       cr = tr.x, dr = tr.y, cg = tg.x, dg = tg.y, cb = tb.x, db = tb.y;
-#else   // A/B: the per-pixel statement the table replaces (round 5 before the table)
-      auto q8f = [&](float x) -> float {
-        const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        return floorf(fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff));
-      };
-      float sr = q8f(r) * F.inv255 * F.nm1, sg = q8f(gg) * F.inv255 * F.nm1, sb = q8f(bl) * F.inv255 * F.nm1;
-      asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
-      dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
-      cr = sr - dr, cg = sg - dg, cb = sb - db;
-#endif
     } else {
       float sr, sg, sb;
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, K.x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
-#if H2S_EXPCLAMP
       // lut3d's clamp to [0, N-1] (NaN -> 0) as the exp's output clamp:
       // x^(1/2.4) clamped to [0, 1] (v_exp_f32 ... clamp; a NaN from the log
       // of a negative or NaN x clamps to 0), then N - 1 times that.  s may
@@ -570,11 +537,6 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       sr = __builtin_amdgcn_fmed3f(fexp2(flog2(r) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
       sg = __builtin_amdgcn_fmed3f(fexp2(flog2(gg) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
       sb = __builtin_amdgcn_fmed3f(fexp2(flog2(bl) * (1.0f / 2.4f)), 0.0f, 1.0f) * K.nm1;
-#else
-      sr = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(r, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
-      sg = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(gg, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
-      sb = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(bl, 0.0f, K.x_max)), 1.0f / 2.4f, K.log2_nm1));
-#endif
       // s is a product when N-1 is not a power of two (N-1 times the clamped
       // power): without this barrier the compiler contracts the cell origin
       // s - fract(s) below into fma(N-1, x, -fract(s)), which carries the
@@ -585,7 +547,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
       cr = sr - dr, cg = sg - dg, cb = sb - db;
     }
-    const int base = (int)fmaf(cb, K.stride_b, fmaf(cg, K.stride_g, cr * (H2S_CELL_LAYOUT ? K.stride_r : 12.0f)));
+    const int base = (int)fmaf(cb, K.stride_b, fmaf(cg, K.stride_g, cr * 12.0f));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
     // fractions: the 4 low mantissa bits of each fraction carry its axis a
     // (bits 3:2 and 1:0 both = a; r 0, g 1, b 2; a change of <= 2^-19
@@ -633,9 +595,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
         // contracted into v_fmac under hipcc's default fp-contract=fast until
         // round 5: the pragma is what keeps the products rounded)
         auto ch = [&](float a, float b, float c, float d) {
-#if !H2S_LP_BLEND_FUSED
 #pragma clang fp contract(off)
-#endif
           return ((w0 * a + w1 * b) + w2 * c) + w3 * d;
         };
         return f3{ch(c0.x, c1.x, c2.x, c3.x), ch(c0.y, c1.y, c2.y, c3.y), ch(c0.z, c1.z, c2.z, c3.z)};
@@ -681,34 +641,6 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       };
       o = blend(sl(b0), sl(b0 + m0), sl(b0 + n0), sl(b0 + F.c111));
     } else {
-#if H2S_LDS_BOX
-      // A/B: the LDS-staged lattice box.  When every
-      // lane's cell lies within one cell of lane 0's, the wave loads the 4 x 4
-      // x 4 nodes around it with ONE gather (lane l: node l) into its 768-B
-      // LDS box and reads the four corners from there, instead of four
-      // gathers.  Same records, same blend: bit-identical
-      bool boxed = false;
-      if constexpr (TAG) {
-        auto rfl = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
-        const float xr = cr - rfl(cr) + 1.0f, xg = cg - rfl(cg) + 1.0f, xb = cb - rfl(cb) + 1.0f;
-        const bool fit = xr == __builtin_amdgcn_fmed3f(xr, 0.0f, 2.0f) && xg == __builtin_amdgcn_fmed3f(xg, 0.0f, 2.0f) &&
-                         xb == __builtin_amdgcn_fmed3f(xb, 0.0f, 2.0f);
-        if (__builtin_amdgcn_ballot_w64(!fit) == 0 && __builtin_amdgcn_read_exec() == ~0ull) {
-          const int ba = __builtin_amdgcn_readfirstlane(base);
-          const f3 nd = __builtin_amdgcn_raw_buffer_load_b96(lut, ba + K.boxofs, 0, 0);   // out of range -> 0 (unused nodes)
-          const int l3 = 3 * (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
-          K.box[l3] = nd.x, K.box[l3 + 1] = nd.y, K.box[l3 + 2] = nd.z;
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          const int bi = 3 * (int)fmaf(xb, 16.0f, fmaf(xg, 4.0f, xr));      // corner 0, in floats
-          const int omb = 3 << (amax >> 1), ocnb = 63 - (3 << ((umin & 12u) >> 1));   // +1 node: 3 / 12 / 48 floats
-          auto rd = [&](int i) { return f3{K.box[i], K.box[i + 1], K.box[i + 2]}; };
-          o = blend(rd(bi), rd(bi + omb), rd(bi + ocnb), rd(bi + 63));
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // reads done before the next step's writes
-          boxed = true;
-        }
-      }
-      if (!boxed)
-#endif
       o = blend(__builtin_amdgcn_raw_buffer_load_b96(lut, base, 0, 0), __builtin_amdgcn_raw_buffer_load_b96(lut, base + om, 0, 0),
                 __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0),
                 __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0));
@@ -842,20 +774,6 @@ __device__ __forceinline__ TileGeo tile_geo(const FastParams& F, unsigned tile) 
   g.f = (int)(bt / F.nby);
   const int by = (int)(bt % F.nby);
   g.px0 = (int)bx * TBW, g.py0 = by * TBH, g.cx0 = (int)bx * CBW, g.cy0 = by * CBH;
-  return g;
-}
-
-// A/B (H2S_PATCH_WALK): a block's 8 tiles as a 4 x 2 patch (256 x 64
-// pixels) instead of a 1 x 8 row (512 x 32): tile t -> patch t / 8, tile t % 8
-// at (t % 4, t / 4 % 2) within it; patches in x, then y, then frame order.
-// Needs nbx % 4 == 0, nby % 2 == 0 and 8 tiles per block
-__device__ __forceinline__ TileGeo tile_geo_patch(const FastParams& F, unsigned tile) {
-  const unsigned st = tile >> 3, w = tile & 7u, sbx = F.nbx >> 2, sby = F.nby >> 1;
-  const unsigned sx = st % sbx, r = st / sbx;
-  const unsigned bx = 4 * sx + (w & 3u), by = 2 * (r % sby) + (w >> 2);
-  TileGeo g;
-  g.f = (int)(r / sby);
-  g.px0 = (int)bx * TBW, g.py0 = (int)by * TBH, g.cx0 = (int)bx * CBW, g.cy0 = (int)by * CBH;
   return g;
 }
 
@@ -1067,7 +985,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
-  __shared__ float lbox[H2S_LDS_BOX && !LP ? 4 * 192 : 1];   // H2S_LDS_BOX: one 64-node box per wave
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -1079,12 +996,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const unsigned tend = tile + (unsigned)F.tpb < ntiles ? tile + (unsigned)F.tpb : ntiles;
 
   // ---- prologue: first tile + tables, all issued before any wait ----
-#if H2S_PATCH_WALK
-  const bool patch = (F.nbx & 3u) == 0 && (F.nby & 1u) == 0 && F.tpb == 8;   // block-uniform
-  TileGeo geo = patch ? tile_geo_patch(F, tile) : tile_geo(F, tile);
-#else
   TileGeo geo = tile_geo(F, tile);
-#endif
   const LaneOfs lofs = lane_ofs(F, t);
   TileRegs cur = tile_load(F, geo, t, lofs);
   const __amdgpu_buffer_rsrc_t req = __builtin_amdgcn_make_buffer_rsrc((void*)F.eq_lut, (short)0, 2 * F.eq_n, 0x00020000);
@@ -1146,10 +1058,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
-  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, in_vgpr(F.stride_r), og, ob, ocr, ocg, ocb, log2_nm1, x_max,
-                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab,
-                lbox + (H2S_LDS_BOX && !LP ? 192 * w : 0),
-                ((lane & 3) - 1) * 12 + (((lane >> 2) & 3) - 1) * og + ((lane >> 4) - 1) * ob};
+  const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
+                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab};
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
@@ -1221,11 +1131,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
     const TileGeo g = geo;
     const bool more = tile + 1 < tend;   // block-uniform
     if (more) {
-#if H2S_PATCH_WALK
-      if (patch)
-        geo = tile_geo_patch(F, tile + 1);
-      else
-#endif
       tile_next(F, geo);
       cur = tile_load(F, geo, t, lofs);  // in flight during this tile's compute
     }
