@@ -23,6 +23,7 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
 hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s);
 hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
+hipError_t build_lut8x(const float4* lut, int n, unsigned* out, int morton, hipStream_t s);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, long long sfp, uint8_t* dst, int ow,
                             int oh, long long dls, long long dfp, const float* wx, const int* sx, const float* wy,
                             const int* sy, int T, int nframes, hipStream_t s);
@@ -53,6 +54,9 @@ struct h2s_ctx {
   float* d_lut_yuv = nullptr;  // lattice pre-multiplied into output code space (3 floats/point)
   float lut_yuv_scale = -1.0f;  // quantiser scale it was built for (-1 = stale)
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
+  unsigned* d_lut8x = nullptr;  // libplacebo branch: lut3d's 8-bit output per rgba code triple (2^24, 64 MiB)
+  bool lut8x_ok = false;        // built for the current lattice
+  int lut8x_morton = 1;         // its order (H2S_LP_TAB=0 in the environment: linear, A/B)
   bool fast_enabled = true;
   bool lp_exact = false;  // H2S_OPT_LP_EXACT
   int peak_blocks = h2s::PEAK_BLOCKS;   // H2S_OPT_TEST_PEAK_BLOCKS (private A/B hook)
@@ -653,6 +657,7 @@ int h2s_create(int device, h2s_ctx** out) {
   c->device = device;
   h2s_params_default(&c->params);
   if (const char* v = getenv("H2S_HOST_SERIAL")) c->serial_host = atoi(v) != 0;
+  if (const char* v = getenv("H2S_LP_TAB")) c->lut8x_morton = atoi(v) != 0;
   if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
     const int tpb = atoi(v);
     if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
@@ -668,6 +673,7 @@ void h2s_destroy(h2s_ctx* c) {
   if (c->aux) {  // the lattices are stream-ordered allocations of the context stream
     if (c->d_lut) hipFreeAsync(c->d_lut, c->aux);
     if (c->d_lut_yuv) hipFreeAsync(c->d_lut_yuv, c->aux);
+    if (c->d_lut8x) hipFreeAsync(c->d_lut8x, c->aux);
     hipStreamSynchronize(c->aux);
     hipStreamDestroy(c->aux);
   }
@@ -793,6 +799,7 @@ int h2s_set_lut(h2s_ctx* c, const float* rgb, int n) {
     c->d_lut_yuv = nullptr;
   }
   c->lut_yuv_scale = -1.0f;
+  c->lut8x_ok = false;
   if (!c->d_lut) {
     hipError_t e = hipMallocAsync((void**)&c->d_lut, cnt * sizeof(float4), aux);
     if (e != hipSuccess) {
@@ -949,6 +956,8 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->cb = F->c111 - F->ob;
   F->lut_yuv = c->d_lut_yuv;
   F->lut_bytes = 12 * n * n * n;
+  F->lut8x = c->d_lut8x;
+  F->lp_tab_morton = c->lut8x_morton;
   F->eq_lut = c->d_eq;
   F->eq_n = k.qmax + 1;
   F->c_bias = 128.0f * k.qscale + 0.5f;
@@ -962,7 +971,28 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->pq_tab = p->transfer_in == H2S_TRC_HLG && k.pipe != h2s::PIPE_LIBPLACEBO ? c->d_hlg : c->d_pq;
 }
 
+// the libplacebo branch's lut3d 8-bit table (k_build_lut8x): allocated on
+// the context stream once, rebuilt on s after every h2s_set_lut
+static int ensure_lut8x(h2s_ctx* c, hipStream_t s) {
+  if (c->d_lut8x && c->lut8x_ok) return 0;
+  if (!c->d_lut8x) {
+    hipStream_t aux;
+    if (int rc = aux_stream(c, &aux)) return rc;
+    hipError_t e = hipMallocAsync((void**)&c->d_lut8x, sizeof(unsigned) << 24, aux);
+    if (e == hipSuccess) e = hipStreamSynchronize(aux);
+    if (e != hipSuccess) {
+      c->d_lut8x = nullptr;
+      return fail(c, H2S_E_OOM, "lut3d 8-bit table allocation failed");
+    }
+  }
+  hipError_t e = h2s::build_lut8x(c->d_lut, c->lut_n, c->d_lut8x, c->lut8x_morton, s);
+  if (e != hipSuccess) return hip_fail(c, e, "lut3d 8-bit table build");
+  c->lut8x_ok = true;
+  return 0;
+}
+
 static int ensure_lut_yuv(h2s_ctx* c, const KParams& k, hipStream_t s) {
+  if (k.rgba8) return ensure_lut8x(c, s);   // the libplacebo branch reads only its 8-bit table
   if (c->d_lut_yuv && c->lut_yuv_scale == k.qscale && c->lut_yuv_rgb == k.rgba8) return 0;
   const size_t cnt = (size_t)c->lut_n * c->lut_n * c->lut_n;
   if (!c->d_lut_yuv) {  // beside d_lut: stream-ordered on the context stream, complete before s uses it
@@ -1149,7 +1179,9 @@ static bool fast_params_ok(const h2s_ctx* c, const KParams& k) {
   // the LUT off runs on the tile kernel for the libplacebo branch only (the
   // CPU chain's legacy closed form stays on the generic kernel)
   if (!k.lut_enabled && k.pipe != h2s::PIPE_LIBPLACEBO) return false;
-  if (k.lut_enabled && c->lut_n > 177) return false;
+  // the CPU chain forms lattice byte offsets in float32 (exact to N = 177);
+  // the libplacebo branch reads its 8-bit table, any N
+  if (k.lut_enabled && c->lut_n > 177 && !k.rgba8) return false;
   if (k.lut_in16) return false;
   // BICUBIC: the tile kernel runs pass 1 frame by frame (not under dynamic peak detection)
   if (p.chroma_filter == H2S_CHROMA_BICUBIC && p.peak_detect) return false;

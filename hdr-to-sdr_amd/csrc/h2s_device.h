@@ -201,6 +201,9 @@ struct FastParams : CurveConsts {
   int og, ob, cr, cg, cb, c111;                // corner byte offsets
   const float* lut_yuv;                        // 12-byte records (Y', Cb', Cr')
   int lut_bytes;
+  int lp_tab_morton;                           // lut8x order: 0 index r | g << 8 | b << 16, 1 bit-interleaved
+  const unsigned* lut8x;                       // libplacebo branch: lut3d's 8-bit output per rgba code triple
+                                               // (index r | g << 8 | b << 16; R | G << 8 | B << 16), k_build_lut8x
   // S6..S8
   const uint16_t* eq_lut;
   int eq_n;

@@ -863,6 +863,42 @@ hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakSta
   return hipGetLastError();
 }
 
+// The libplacebo branch's lut3d 8-bit table for the tile kernel: for every
+// rgba8 code triple (r, g, b), lut3d's 8-bit output -- coordinate (q / 255)
+// (N-1), tetrahedral blend, truncation -- in this translation unit's
+// arithmetic (no FMA contraction: the oracle's lut3d_8bit order, as
+// chain_px / lpx_chain), packed R | G << 8 | B << 16.  2^24 entries, 64 MiB;
+// built once per lattice (h2s_api.hip ensure_lut8x)
+// morton: the entries in bit-interleaved order (index bit 3k = r bit k, 3k+1
+// = g bit k, 3k+2 = b bit k), so that a 128-byte line holds a 4 x 4 x 2
+// block of codes
+__global__ __launch_bounds__(256) void k_build_lut8x(const KParams P, unsigned* out, int morton) {
+  const unsigned i = blockIdx.x * 256 + threadIdx.x;
+  unsigned cr = i & 255, cg = (i >> 8) & 255, cb = i >> 16;
+  if (morton) {
+    cr = cg = cb = 0;
+    for (int k = 0; k < 8; k++) {
+      cr |= ((i >> (3 * k)) & 1u) << k;
+      cg |= ((i >> (3 * k + 1)) & 1u) << k;
+      cb |= ((i >> (3 * k + 2)) & 1u) << k;
+    }
+  }
+  const float sf = 1.0f / 255.0f;
+  float r = (float)cr * sf, g = (float)cg * sf, b = (float)cb * sf;
+  lut3d_tetra(P, r, g, b);
+  const unsigned R = (unsigned)fminf(fmaxf(truncf(r * 255.0f), 0.0f), 255.0f);
+  const unsigned G = (unsigned)fminf(fmaxf(truncf(g * 255.0f), 0.0f), 255.0f);
+  const unsigned B = (unsigned)fminf(fmaxf(truncf(b * 255.0f), 0.0f), 255.0f);
+  out[i] = R | (G << 8) | (B << 16);
+}
+
+hipError_t build_lut8x(const float4* lut, int n, unsigned* out, int morton, hipStream_t s) {
+  KParams P{};
+  P.lut = lut, P.lut_n = n, P.lut_sg = n, P.lut_sb = n * n, P.lut_max = (float)(n - 1);
+  hipLaunchKernelGGL(k_build_lut8x, dim3((1u << 24) / 256), dim3(256), 0, s, P, out, morton);
+  return hipGetLastError();
+}
+
 // device libm_powf / libm_expf over n inputs (fn 0: powf(x, y), 1: expf(x)),
 // for tests/test_libm_tables.py's bit-equality check against the libm the
 // oracle links

@@ -431,7 +431,7 @@ struct StepK {
 // debug planes (DBG > 0, frame 0), else -1.
 template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
-                                             const float4* pqi_lds, const uint16_t* eq_lds, const float2* lut8_lds,
+                                             const float4* pqi_lds, const uint16_t* eq_lds, __amdgpu_buffer_rsrc_t lut8x, const unsigned* spread_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
                                              long long di, float& oyv, float& ozv, float qoff, float ydq) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
@@ -500,32 +500,50 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
     o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
     o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
+  } else if constexpr (LP) {
+    // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the range=tv
+    // and rounding / dither offsets, h2s_lp_range / _dither; all >= 0, so the
+    // conversion's truncation is the floor).  Everything after the download
+    // -- lut3d's 8-bit coordinate (q / 255) (N-1), the tetrahedral blend in
+    // vf_lut3d's order, the truncation to 8 bits -- is a function of the three
+    // codes alone, so it is one read of the context's 2^24-entry table of
+    // lut3d's 8-bit outputs (k_build_lut8x: the generic kernel's own
+    // lut3d_8bit arithmetic, bit for bit), instead of a lattice cell, four
+    // gathers and the blend per pixel (round 6)
+    auto q8 = [&](float x) -> unsigned {
+      const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
+      return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
+    };
+    if (DBG == 3) {
+      auto ev = [&](float x) {
+        const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
+        return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
+      };
+      dput(ev(r), ev(gg), ev(bl));
+    }
+    unsigned idx;
+    const unsigned qr = q8(r), qg = q8(gg), qb = q8(bl);
+    if (F.lp_tab_morton) {   // bit-interleaved (Morton) order: nearby colours share lines
+      asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(spread_lds[qb]), "v"(spread_lds[qg]));
+      asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(idx), "v"(spread_lds[qr]));
+    } else {
+      asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(idx) : "v"(qb), "v"(qg));
+      asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(idx) : "v"(idx), "v"(qr));
+    }
+    const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(lut8x, idx << 2, 0, 0);
+    const float R = (float)(v & 255u) * F.inv255, G = (float)((v >> 8) & 255u) * F.inv255,
+                B = (float)((v >> 16) & 255u) * F.inv255;
+    if (DBG == 4) dput(R, G, B);
+    // BT.709 limited-range Y'CbCr at depth q in the generic kernel's
+    // operation order; o = (luma code + 0.5, 56 q Cb, 56 q Cr)
+    const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
+    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
+    o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
+    o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
   } else {
     // lattice cell origins (cr, cg, cb) and fractions (dr, dg, db) per channel
     float cr, cg, cb, dr, dg, db;
-    if (LP) {
-      // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the
-      // range=tv and rounding / dither offsets, h2s_lp_range / _dither; all
-      // >= 0, so the conversion's truncation is the floor), then lut3d's
-      // 8-bit coordinate (q / 255) (N-1) in its own operation order, read as
-      // (cell, fraction) from the block's 256-entry table (lut8_lds, made in
-      // the prologue by the same float operations): q = 255 lands on N-1
-      // exactly (fraction 0: the corners past the lattice edge get weight 0
-      // and read in-bounds records or the buffer's zero fill)
-      auto q8 = [&](float x) -> unsigned {
-        const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-        return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
-      };
-      if (DBG == 3) {
-        auto ev = [&](float x) {
-          const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-          return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
-        };
-        dput(ev(r), ev(gg), ev(bl));
-      }
-      const float2 tr = lut8_lds[q8(r)], tg = lut8_lds[q8(gg)], tb = lut8_lds[q8(bl)];
-      cr = tr.x, dr = tr.y, cg = tg.x, dg = tg.y, cb = tb.x, db = tb.y;
-    } else {
+    {
       float sr, sg, sb;
       // S3+S4: s = (N-1) x^(1/2.4) with x clamped to [0, K.x_max] (NaN -> 0), so
       // s < N-1 and the lattice cell index never needs a clamp
@@ -556,11 +574,10 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     // the axes of the largest and smallest; the corner offsets come from a
     // 3-entry LDS table (om = +1 along the max axis, ocn = the far corner less
     // the min axis), not from compares and selects (9 half-rate VALU ops ->
-    // 3).  Not on the libplacebo branch: its 8-bit coordinates make exact ties
-    // between fractions common, and lut3d's truncating 8-bit output turns the
-    // tags' perturbation of a tie into a flipped code (1.3 % of a ramp's
-    // pixels)
-    constexpr bool TAG = H2S_TAGSEL && !LP;
+    // 3).  (Not for the libplacebo branch's 8-bit coordinates, whose exact
+    // ties between fractions the tags would break: that branch reads its
+    // table above.)
+    constexpr bool TAG = H2S_TAGSEL;
     int om, ocn;
     float dmax, dmin, dmid;
     unsigned umin = 0, amax = 0;
@@ -587,32 +604,16 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     }
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     auto blend = [&](const f3 c0, const f3 c1, const f3 c2, const f3 c3) {
-      if constexpr (LP) {
-        // lut3d's 8-bit path truncates its output to 8 bits: the blend in
-        // the oracle's (vf_lut3d C) order, products and sums each rounded (no
-        // FMA), so that a blend on an integer boundary truncates alike.
-        // (__fmul_rn / __fadd_rn are plain operators in HIP and were being
-        // contracted into v_fmac under hipcc's default fp-contract=fast until
-        // round 5: the pragma is what keeps the products rounded)
-        auto ch = [&](float a, float b, float c, float d) {
-#pragma clang fp contract(off)
-          return ((w0 * a + w1 * b) + w2 * c) + w3 * d;
-        };
-        return f3{ch(c0.x, c1.x, c2.x, c3.x), ch(c0.y, c1.y, c2.y, c3.y), ch(c0.z, c1.z, c2.z, c3.z)};
-      }
       f3 r = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
       // the luma quantiser's ordered-dither offset (ydq = d - 0.5, 0 without
-      // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL);
-      // on the libplacebo branch o.x is lut3d's R, and the dither belongs to
-      // the luma quantiser below
-      r.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, LP ? 0.0f : ydq))));
+      // dither: the record's +0.5 rounds) as the blend's first term (FMA for MUL)
+      r.x = fmaf(w3, c3.x, fmaf(w2, c2.x, fmaf(w1, c1.x, fmaf(w0, c0.x, ydq))));
       return r;
     };
-    // CPU chain: when every lane of the step is in one cell and one
-    // tetrahedron, its four records come through the scalar cache and the
-    // step issues no vector-memory gather (bit-identical; C2 -1.8 % smooth,
-    // -5 % on the website frame; the libplacebo instances measured +8 %,
-    // SGPR-bound, and keep the gathers: profiles/r03/ablations/sgather_*.log)
+    // when every lane of the step is in one cell and one tetrahedron, its
+    // four records come through the scalar cache and the step issues no
+    // vector-memory gather (bit-identical; C2 -1.8 % smooth, -5 % on the
+    // website frame: profiles/r03/ablations/sgather_*.log)
     bool step_uniform;
     int b0, m0, n0;
     if constexpr (TAG) {
@@ -630,7 +631,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     } else {
       b0 = __builtin_amdgcn_readfirstlane(base), m0 = __builtin_amdgcn_readfirstlane(om),
       n0 = __builtin_amdgcn_readfirstlane(ocn);
-      step_uniform = !LP && __builtin_amdgcn_ballot_w64(base != b0 || om != m0 || ocn != n0) == 0;
+      step_uniform = __builtin_amdgcn_ballot_w64(base != b0 || om != m0 || ocn != n0) == 0;
     }
     if (step_uniform) {
       typedef __attribute__((address_space(4))) const float cfl;
@@ -645,21 +646,8 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
                 __builtin_amdgcn_raw_buffer_load_b96(lut, base + ocn, 0, 0),
                 __builtin_amdgcn_raw_buffer_load_b96(lut, base, F.c111, 0));
     }
-    if (LP) {
-      // lut3d 8-bit output (truncated, clipped), then BT.709 limited-range
-      // Y'CbCr at depth q in the generic kernel's operation order; o = (luma
-      // code + 0.5, 56 q Cb, 56 q Cr) as the Y'CbCr lattice would give
-      const float R = __builtin_amdgcn_fmed3f(truncf(o.x * 255.0f), 0.0f, 255.0f) * F.inv255;
-      const float G = __builtin_amdgcn_fmed3f(truncf(o.y * 255.0f), 0.0f, 255.0f) * F.inv255;
-      const float B = __builtin_amdgcn_fmed3f(truncf(o.z * 255.0f), 0.0f, 255.0f) * F.inv255;
-      if (DBG == 4) dput(R, G, B);
-      const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-      o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
-      o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
-      o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
-    }
-    if (DBG == 3 && !LP) dput((cr + dr) * F.inv_nm1, (cg + dg) * F.inv_nm1, (cb + db) * F.inv_nm1);   // = s exactly
-    if (DBG == 4 && !LP) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
+    if (DBG == 3) dput((cr + dr) * F.inv_nm1, (cg + dg) * F.inv_nm1, (cb + db) * F.inv_nm1);   // = s exactly
+    if (DBG == 4) {  // same cell / corners / weights on the RGB lattice (12-byte record -> float4 index)
       const float4 q0 = F.dbg_lut[base / 12], q1 = F.dbg_lut[(base + om) / 12], q2 = F.dbg_lut[(base + ocn) / 12],
                    q3 = F.dbg_lut[(base + F.c111) / 12];
       dput(w0 * q0.x + w1 * q1.x + w2 * q2.x + w3 * q3.x, w0 * q0.y + w1 * q1.y + w2 * q2.y + w3 * q3.y,
@@ -981,10 +969,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
   __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
-  __shared__ float2 lut8_lds[LP ? 256 : 1];    // lut3d 8-bit coordinate per rgba code: (cell, fraction)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
+  __shared__ unsigned spread_lds[LP ? 256 : 1];   // LP, Morton table order: code c's bits at every third position
   // PQ: E is produced pre-scaled into table-segment units (the x PQ_SEG is
   // folded into the Y'CbCr->R'G'B' constants)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;   // as px_chain
@@ -1022,11 +1010,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   if (stage_pq && t == 255) pq_lds[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < 2) tflag[t] = 0;
   if (t < 3) offtab[t] = t == 0 ? 12 : (t == 1 ? F.og : F.ob);
-  if (LP) {   // (q / 255) (N-1) as px_chain's former per-pixel statement, and its fraction
-    float sq = (float)t * F.inv255 * F.nm1;
-    asm("" : "+v"(sq));   // no contraction of sq - dq into fma(.., F.nm1, -dq): see px_chain
-    const float dq = __builtin_amdgcn_fractf(sq);
-    lut8_lds[t] = make_float2(sq - dq, dq);
+  if (LP) {
+    unsigned x = (unsigned)t;
+    x = (x | (x << 8)) & 0x0F00Fu;
+    x = (x | (x << 4)) & 0x0C30C3u;
+    spread_lds[t] = (x | (x << 2)) & 0x249249u;
   }
   __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
@@ -1082,6 +1070,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
     CurveConsts cv = F;
     if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
     const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
+    // the libplacebo branch's lut3d 8-bit table (2^24 packed R'G'B' codes, 64 MiB)
+    const __amdgpu_buffer_rsrc_t lut8x = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut8x, (short)0, LP ? (1 << 26) : 0, 0x00020000);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
@@ -1096,7 +1086,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut8_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
+          F, cv, pq_lds, pqi_lds, eq_lds, lut8x, spread_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
       if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it

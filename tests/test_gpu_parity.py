@@ -239,15 +239,29 @@ def test_lut_sizes(tm, lut_n):
     assert tm.query_path(src, dst) == (_abi.PATH_TILE if lut_n <= 177 else _abi.PATH_GENERIC)
 
 
-@pytest.mark.parametrize('lut_n', [2, 17, 33, 129, 177])
+@pytest.mark.parametrize('lut_n', [2, 17, 33, 129, 177, 200, 256])
 def test_lut_sizes_libplacebo(tm, lut_n):
     """lut3d's 8-bit path on the libplacebo branch at other lattice sizes:
-    k_tile<..., LP=1> takes each channel's (cell, fraction) from its 256-entry
-    LDS table of (q / 255) (N-1) (h2s_tile.h lut8_lds), N - 1 a power of two
-    or not; the rgba code 255 lands on the last node."""
+    k_tile<..., LP=1> reads lut3d's output for its three rgba codes from the
+    context's 2^24-entry table (k_build_lut8x: (q / 255) (N-1), N - 1 a
+    power of two or not, the code 255 on the last node), so every N up to
+    256 stays on the tile path."""
+    from hdr2sdr import _abi
     params = hdr2sdr.TonemapParams(tonemapper='bt.2390', pipeline='libplacebo')
     got, want, src_wh = run_both(tm, params, 'uniform', 64, 32, lut_n=lut_n)
-    assert_close_int(params, got, want, *src_wh)
+    assert_close_int(params, got, want, *src_wh, lut_n=lut_n)
+    src = hdr2sdr.FrameBatch.empty_torch(1, 64, 32, 10, 'cuda')
+    dst = hdr2sdr.FrameBatch.empty_torch(1, 64, 32, 10, 'cuda')
+    assert tm.query_path(src, dst) == _abi.PATH_TILE
+
+
+def test_lut8x_table_rebuilt_after_set_lut(tm):
+    """The 8-bit table follows the lattice: a new h2s_set_lut (another size,
+    then the first again) changes the branch's output as the oracle's."""
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', pipeline='libplacebo')
+    for n in (33, 65, 33):
+        got, want, src_wh = run_both(tm, params, 'smooth', 128, 64, lut_n=n)
+        assert_close_int(params, got, want, *src_wh, lut_n=n)
 
 
 # 1e-3 relative on the float path (north_star), per stage, on the kernel that
