@@ -531,7 +531,7 @@ def main():
         # gfx950 rate (2 cycles per wave64 full-rate op per SIMD-32, 4 per
         # transcendental), the texture data / address units' busy shares;
         # 'frac' stays the HBM fraction north_star's roofline asks for
-        for k in ('valu_insts_per_cu_cycle', 'valu_issue_frac', 'valu_active_frac', 'td_busy_frac',
+        for k in ('valu_insts_per_cu_cycle', 'valu_issue_frac', 'valu_waves_per_simd', 'td_busy_frac',
                   'td_tc_stall_frac', 'ta_busy_frac'):
             if k in tr:
                 rec['roofline'][k] = tr[k]

@@ -23,7 +23,7 @@ hipError_t launch_fast(const FastParams& F, int trc, int tm, int desat, int lp, 
 hipError_t launch_process_c444(const KParams& P, bool out8, hipStream_t s);
 hipError_t launch_chroma_bicubic(const KParams& P, const float* wx7, const float* wy8, bool out8, hipStream_t s);
 hipError_t build_lut_yuv(const float4* rgb, float* yuv, int n, const YuvLutConsts& K, hipStream_t st);
-hipError_t build_lut8x(const float4* lut, int n, unsigned* out, int morton, hipStream_t s);
+hipError_t build_lut8x(const float4* lut, int n, unsigned* out, hipStream_t s);
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, long long sls, long long sfp, uint8_t* dst, int ow,
                             int oh, long long dls, long long dfp, const float* wx, const int* sx, const float* wy,
                             const int* sy, int T, int nframes, hipStream_t s);
@@ -56,7 +56,6 @@ struct h2s_ctx {
   int lut_yuv_rgb = 0;          // 1: it holds plain R'G'B' records (libplacebo rgba8 form)
   unsigned* d_lut8x = nullptr;  // libplacebo branch: lut3d's 8-bit output per rgba code triple (2^24, 64 MiB)
   bool lut8x_ok = false;        // built for the current lattice
-  int lut8x_morton = 1;         // its order (H2S_LP_TAB=0 in the environment: linear, A/B)
   bool fast_enabled = true;
   bool lp_exact = false;  // H2S_OPT_LP_EXACT
   int peak_blocks = h2s::PEAK_BLOCKS;   // H2S_OPT_TEST_PEAK_BLOCKS (private A/B hook)
@@ -393,11 +392,12 @@ void resolve(const h2s_params* p, KParams* k, std::vector<uint16_t>* eq) {
 
 // ST 2084 inverse EOTF (y = luminance / 10000 -> E) as PQI_NSEG cubic
 // segments for the tile kernel's IPT form (h2s_tile.h pqi): segment s covers
-// y = 2^e (1 + j/4 + t), e = PQI_OCT0 + s/4, j = s%4, t in [0, 1/4), read from
-// the float's exponent and top two mantissa bits; the cubic in t through the
-// exact (double) encode at the 4 Chebyshev nodes.  Max relative error 1.1e-6
-// (near y = 2^-15) with float32 coefficients; below 2^-40 (1e-8 nits) the
-// first segment is used (E < 1.5e-5)
+// y = 2^e (1 + j/8 + t), e = PQI_OCT0 + s/8, j = s%8, t in [0, 1/8), read from
+// the float's exponent and top three mantissa bits; the cubic in t through
+// the exact (double) encode at the 4 Chebyshev nodes (relative error <=
+// 1.5e-7 with float32 coefficients).  Entry 0 is the constant PQ(0), read for
+// y <= 0 and for y below the first octave (2^-64, 1e-15 nits: PQ within 3e-7
+// of PQ(0)); segment s is entry 1 + s (PQI_NTAB entries)
 static void solve_cubic(const double t[4], const double y[4], double c[4]) {
   double A[4][5];
   for (int k = 0; k < 4; k++) {
@@ -420,7 +420,8 @@ static void solve_cubic(const double t[4], const double y[4], double c[4]) {
 
 void build_pqi_table(std::vector<float4>* out) {
   constexpr int K = h2s::PQI_PER_OCT;
-  out->resize(h2s::PQI_NSEG);
+  out->resize(h2s::PQI_NTAB);
+  (*out)[0] = make_float4(0.0f, 0.0f, 0.0f, (float)pq_encode_d(0.0));
   double t[4];
   for (int k = 0; k < 4; k++) t[k] = (1.0 - cos((2 * k + 1) * M_PI / 8.0)) / 2.0 / K;
   for (int sg = 0; sg < h2s::PQI_NSEG; sg++) {
@@ -428,7 +429,7 @@ void build_pqi_table(std::vector<float4>* out) {
     double y[4], c[4];
     for (int k = 0; k < 4; k++) y[k] = pq_encode_d(base * (1.0 + (double)(sg % K) / K + t[k]));
     solve_cubic(t, y, c);
-    (*out)[sg] = make_float4((float)c[3], (float)c[2], (float)c[1], (float)c[0]);
+    (*out)[1 + sg] = make_float4((float)c[3], (float)c[2], (float)c[1], (float)c[0]);
   }
 }
 
@@ -657,7 +658,6 @@ int h2s_create(int device, h2s_ctx** out) {
   c->device = device;
   h2s_params_default(&c->params);
   if (const char* v = getenv("H2S_HOST_SERIAL")) c->serial_host = atoi(v) != 0;
-  if (const char* v = getenv("H2S_LP_TAB")) c->lut8x_morton = atoi(v) != 0;
   if (const char* v = getenv("H2S_TILES_PER_BLOCK")) {
     const int tpb = atoi(v);
     if (tpb >= 1 && tpb <= 64) c->tiles_per_block = tpb;
@@ -932,6 +932,12 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->lp_ipt = k.lp_ipt;
   F->lp_qs_f = k.lp_qs / 255.0f;
   F->lp_qo = k.lp_qo;
+  for (int i = 0; i < 3; i++) {
+    F->lp_ky[i] = (float)((double)k.k709[i] / 255.0 * 219.0 * (double)k.qscale);
+    F->lp_kcb[i] = (float)((double)k.kcb[i] / 255.0 * 56.0 * (double)k.qscale);
+    F->lp_kcr[i] = (float)((double)k.kcr[i] / 255.0 * 56.0 * (double)k.qscale);
+  }
+  F->lp_cy = 16.0f * k.qscale + 0.5f;
   F->lp_dith = k.lp_dith;
   F->in_mask2 = k.in_mask | (k.in_mask << 16);
   for (int i = 0; i < 9; i++)
@@ -957,7 +963,6 @@ static void resolve_fast(const h2s_ctx* c, const KParams& k, FastParams* F) {
   F->lut_yuv = c->d_lut_yuv;
   F->lut_bytes = 12 * n * n * n;
   F->lut8x = c->d_lut8x;
-  F->lp_tab_morton = c->lut8x_morton;
   F->eq_lut = c->d_eq;
   F->eq_n = k.qmax + 1;
   F->c_bias = 128.0f * k.qscale + 0.5f;
@@ -985,7 +990,7 @@ static int ensure_lut8x(h2s_ctx* c, hipStream_t s) {
       return fail(c, H2S_E_OOM, "lut3d 8-bit table allocation failed");
     }
   }
-  hipError_t e = h2s::build_lut8x(c->d_lut, c->lut_n, c->d_lut8x, c->lut8x_morton, s);
+  hipError_t e = h2s::build_lut8x(c->d_lut, c->lut_n, c->d_lut8x, s);
   if (e != hipSuccess) return hip_fail(c, e, "lut3d 8-bit table build");
   c->lut8x_ok = true;
   return 0;

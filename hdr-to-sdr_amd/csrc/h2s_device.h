@@ -186,6 +186,11 @@ struct FastParams : CurveConsts {
   float lp_qs_f, lp_qo;
   int lp_dith;
   unsigned in_mask2;
+  // the Y'CbCr rows applied to lut3d's 8-bit output codes directly (tile
+  // kernel, round 6): o = (sum lp_ky[c] code_c + lp_cy, sum lp_kcb[c] code_c,
+  // sum lp_kcr[c] code_c), i.e. k709 / kcb / kcr x inv255 x (219 qscale | 56
+  // qscale) folded on the host; lp_cy = 16 qscale + 0.5
+  float lp_ky[3], lp_kcb[3], lp_kcr[3], lp_cy;
   float ipt_r2l[9], ipt_l2r[9];
   const float4* pqi_tab;
   // libplacebo branch with the LUT off (k_tile<..., LP = 1>): libplacebo's own
@@ -201,9 +206,8 @@ struct FastParams : CurveConsts {
   int og, ob, cr, cg, cb, c111;                // corner byte offsets
   const float* lut_yuv;                        // 12-byte records (Y', Cb', Cr')
   int lut_bytes;
-  int lp_tab_morton;                           // lut8x order: 0 index r | g << 8 | b << 16, 1 bit-interleaved
   const unsigned* lut8x;                       // libplacebo branch: lut3d's 8-bit output per rgba code triple
-                                               // (index r | g << 8 | b << 16; R | G << 8 | B << 16), k_build_lut8x
+                                               // (bit-interleaved index; R | G << 8 | B << 16), k_build_lut8x
   // S6..S8
   const uint16_t* eq_lut;
   int eq_n;
@@ -237,6 +241,9 @@ constexpr float PQ_EMAX = 1.875f;    // above: exact transcendental path
 constexpr int PQI_OCT0 = -64;        // PQ encode table: first octave 2^-64 (x 10000 nits)
 constexpr int PQI_PER_OCT = 8;       // segments per octave (exponent + top 3 mantissa bits)
 constexpr int PQI_NSEG = 78 * PQI_PER_OCT;   // octaves 2^-64 .. 2^14
+// the table holds PQI_NSEG + 1 entries: [0] = PQ(0) as a constant (y <= 0,
+// and y below the first octave), [1 + s] = segment s
+constexpr int PQI_NTAB = PQI_NSEG + 1;
 
 struct YuvLutConsts {
   float s, k709[3], kcb[3], kcr[3];

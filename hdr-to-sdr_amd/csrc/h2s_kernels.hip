@@ -869,19 +869,18 @@ hipError_t launch_peak_curves(double2* fstat, int n, const PeakModel& M, PeakSta
 // arithmetic (no FMA contraction: the oracle's lut3d_8bit order, as
 // chain_px / lpx_chain), packed R | G << 8 | B << 16.  2^24 entries, 64 MiB;
 // built once per lattice (h2s_api.hip ensure_lut8x)
-// morton: the entries in bit-interleaved order (index bit 3k = r bit k, 3k+1
-// = g bit k, 3k+2 = b bit k), so that a 128-byte line holds a 4 x 4 x 2
-// block of codes
-__global__ __launch_bounds__(256) void k_build_lut8x(const KParams P, unsigned* out, int morton) {
+// The entries are in bit-interleaved (Morton) order -- index bit 3k = r bit
+// k, 3k+1 = g bit k, 3k+2 = b bit k -- so that a 128-byte line holds a 4 x 4
+// x 2 block of codes (the order r | g << 8 | b << 16 measured up to 42 %
+// slower on smooth content: profiles/r06/lp_table/, patch in
+// profiles/r06/ab_patches/lp_tab_linear.patch)
+__global__ __launch_bounds__(256) void k_build_lut8x(const KParams P, unsigned* out) {
   const unsigned i = blockIdx.x * 256 + threadIdx.x;
-  unsigned cr = i & 255, cg = (i >> 8) & 255, cb = i >> 16;
-  if (morton) {
-    cr = cg = cb = 0;
-    for (int k = 0; k < 8; k++) {
-      cr |= ((i >> (3 * k)) & 1u) << k;
-      cg |= ((i >> (3 * k + 1)) & 1u) << k;
-      cb |= ((i >> (3 * k + 2)) & 1u) << k;
-    }
+  unsigned cr = 0, cg = 0, cb = 0;
+  for (int k = 0; k < 8; k++) {
+    cr |= ((i >> (3 * k)) & 1u) << k;
+    cg |= ((i >> (3 * k + 1)) & 1u) << k;
+    cb |= ((i >> (3 * k + 2)) & 1u) << k;
   }
   const float sf = 1.0f / 255.0f;
   float r = (float)cr * sf, g = (float)cg * sf, b = (float)cb * sf;
@@ -892,10 +891,10 @@ __global__ __launch_bounds__(256) void k_build_lut8x(const KParams P, unsigned* 
   out[i] = R | (G << 8) | (B << 16);
 }
 
-hipError_t build_lut8x(const float4* lut, int n, unsigned* out, int morton, hipStream_t s) {
+hipError_t build_lut8x(const float4* lut, int n, unsigned* out, hipStream_t s) {
   KParams P{};
   P.lut = lut, P.lut_n = n, P.lut_sg = n, P.lut_sb = n * n, P.lut_max = (float)(n - 1);
-  hipLaunchKernelGGL(k_build_lut8x, dim3((1u << 24) / 256), dim3(256), 0, s, P, out, morton);
+  hipLaunchKernelGGL(k_build_lut8x, dim3((1u << 24) / 256), dim3(256), 0, s, P, out);
   return hipGetLastError();
 }
 

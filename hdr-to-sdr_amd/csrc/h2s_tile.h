@@ -50,6 +50,21 @@
 #ifndef H2S_EQMAGIC
 #define H2S_EQMAGIC 1
 #endif
+// Stage markers for the per-stage slot table (scripts/isa_stages.py): in a
+// marked build (-DH2S_ISA_MARKS, ISA listing only, never linked) each is an
+// assembler comment ";@@name" that opens stage `name` in the listing, with a
+// scheduling barrier so that no instruction crosses it; the product build
+// defines them away
+#ifdef H2S_ISA_MARKS
+#define H2S_MARK(name)                  \
+  do {                                  \
+    __builtin_amdgcn_sched_barrier(0);  \
+    asm volatile(";@@" name);           \
+    __builtin_amdgcn_sched_barrier(0);  \
+  } while (0)
+#else
+#define H2S_MARK(name)
+#endif
 
 namespace h2s {
 
@@ -123,26 +138,32 @@ __device__ __forceinline__ float pq_z_dark(const float4* tab, float u, float log
 
 // ST 2084 inverse EOTF of y = luminance / 10000 >= 0 from the LDS table
 // (build_pqi_table): the segment is the float's exponent and top three
-// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); clamped to the
-// table's octaves 2^-64 .. 2^14 (the IPT form caps its input at 1e6 npl;
-// below 2^-64, 1e-15 nits, the first segment's value is within 3e-7 of PQ(0)).
+// mantissa bits, t the remaining 20 mantissa bits as [0, 1/8); the bit
+// pattern is clamped (as a signed integer) to the table's octaves 2^-64 ..
+// 2^14, where one pattern below the first octave reads entry 0, the constant
+// PQ(0) = c1^m2: y <= 0 (black, or an LMS row of a saturated colour) exactly
+// as the oracle's max(y, 0), and y below 2^-64 (1e-15 nits, within 3e-7 of
+// PQ(0)).  The IPT form caps its input at 1e6 npl, inside the top octave.
 // The near-black octaves matter: an LMS row of a dark pixel on synthetic
 // content reaches 1e-13, and clamping at 2^-40 (PQ 1.4e-5 instead of down to
-// 7.3e-7) put 0.5 % errors on stage-2 values of 1e-5.  y <= 0 (black, or an
-// LMS row of a saturated colour) is PQ(0) = c1^m2 exactly, as the oracle's
-// max(y, 0).  Eight segments per octave, not four (round 5): the LMS encode
-// error the decode amplifies (x ~11-45 through the EOTF's slope) drops from
-// ~1e-6 to the float32 floor (scripts/c3_table_flips.py: the rgba8 download
-// flips this table alone causes drop 7x); the 10 KB table puts the libplacebo
-// instances above 32 KB of LDS, i.e. at 4 blocks per CU
+// 7.3e-7) put 0.5 % errors on stage-2 values of 1e-5.  Eight segments per
+// octave, not four (round 5): the LMS encode error the decode amplifies (x
+// ~11-45 through the EOTF's slope) drops from ~1e-6 to the float32 floor
+// (scripts/c3_table_flips.py: the rgba8 download flips this table alone
+// causes drop 7x); the 10 KB table puts the libplacebo instances above 32 KB
+// of LDS, i.e. at 4 blocks per CU.  Round 6: 8 VALU instructions (integer
+// med3, bfe, shift-add, and-or, add, 3 FMA) instead of 13 -- the clamp on the
+// pattern replaces the segment clamp and the y <= 0 select
 __device__ __forceinline__ float pqi(const float4* tab, float y) {
-  const int yi = (int)__builtin_bit_cast(unsigned, y);
-  const unsigned b = (unsigned)max(yi, 0);
-  const int sg = min(max((int)(b >> 20) - ((127 + PQI_OCT0) << 3), 0), PQI_NSEG - 1);
-  const float t = __builtin_bit_cast(float, (b & 0xFFFFFu) | 0x3F800000u) - 1.0f;
-  const float4 c = tab[sg];
-  const float v = fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
-  return yi > 0 ? v : 7.309559e-07f;
+  constexpr int S0 = (127 + PQI_OCT0) << 3;                  // absolute segment of 2^-64
+  constexpr int LO = (S0 - 1) << 20;                         // reads entry 0
+  constexpr int HI = ((S0 + PQI_NSEG) << 20) - 1;            // the top segment's last pattern
+  const int bc = min(max(__builtin_bit_cast(int, y), LO), HI);   // (v_med3_i32)
+  unsigned sa;
+  asm("v_bfe_u32 %0, %1, 20, 11" : "=v"(sa) : "v"(bc));      // absolute segment (sign bit is 0)
+  const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + ((sa - (unsigned)(S0 - 1)) << 4));
+  const float t = __builtin_bit_cast(float, ((unsigned)bc & 0xFFFFFu) | 0x3F800000u) - 1.0f;
+  return fmaf(fmaf(fmaf(c.x, t, c.y), t, c.z), t, c.w);
 }
 
 // S1 transfer to linear (units of npl), specialised
@@ -322,12 +343,15 @@ __device__ __forceinline__ void tone(const FastParams& F, const CurveConsts& C, 
       // the intensity of IPT-PQ with P and T kept, i.e. L'M'S' += I' - I;
       // encode and decode through the LDS tables (launch-uniform branch; the
       // EOTF table is staged for HLG input too)
+      H2S_MARK("S2a RGB->LMS, PQ encode x3");
       const float R = fminf(r, 1e6f), G = fminf(g, 1e6f), B = fminf(b, 1e6f);
       const float q0 = pqi(pqi_lds, F.ipt_r2l[0] * R + F.ipt_r2l[1] * G + F.ipt_r2l[2] * B);
       const float q1 = pqi(pqi_lds, F.ipt_r2l[3] * R + F.ipt_r2l[4] * G + F.ipt_r2l[5] * B);
       const float q2 = pqi(pqi_lds, F.ipt_r2l[6] * R + F.ipt_r2l[7] * G + F.ipt_r2l[8] * B);
+      H2S_MARK("S2b I, curve");
       const float I = 0.4f * q0 + 0.4f * q1 + 0.2f * q2;
       const float du = curve_u(I) - I * (float)PQ_SEG;   // (I' - I) PQ_SEG + 1
+      H2S_MARK("S2c EOTF x3, LMS->RGB");
       auto lz = [&](float q) { return pz(__builtin_amdgcn_fmed3f(fmaf(q, (float)PQ_SEG, du), 1.0f, PQZ_LIM - 0.01f)); };
       const float l0 = lz(q0), l1 = lz(q1), l2 = lz(q2);
       r = F.ipt_l2r[0] * l0 + F.ipt_l2r[1] * l1 + F.ipt_l2r[2] * l2;
@@ -422,6 +446,7 @@ struct StepK {
   int c111;                       // the far corner's byte offset
   float nm1;                      // N - 1
   const int* offtab;              // LDS: byte offset of the +1 corner along r, g, b at bytes 0, 4, 8
+  float lp_k2, lp_hi, lp_cy;      // LP: the encode's clamp bounds lp_k2, 255 + lp_k2; lp_cy + ydq
 };
 
 // One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
@@ -431,18 +456,21 @@ struct StepK {
 // debug planes (DBG > 0, frame 0), else -1.
 template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
 __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
-                                             const float4* pqi_lds, const uint16_t* eq_lds, __amdgpu_buffer_rsrc_t lut8x, const unsigned* spread_lds,
+                                             const float4* pqi_lds, const uint16_t* eq_lds, const unsigned* lut8v, const unsigned* spread_lds,
                                              __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
                                              long long di, float& oyv, float& ozv, float qoff, float ydq) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
   // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
   constexpr bool EQM = H2S_EQMAGIC && !LP;   // see the eq lookup at the end
+  H2S_MARK("S1a E");
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
   const float eb = fmaf(U, K.a_bu, ybs);
   float r, gg, bl;
+  H2S_MARK("S1b EOTF");
   const bool safe = to_linear<TRC, ESC, NOEX>(F, pq_lds, er, eg, eb, r, gg, bl);
+  H2S_MARK("S2 tone");
   const long long dpl = (long long)F.dbg_w * F.H;
   auto dput = [&](float a, float b_, float c) {
     if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
@@ -461,6 +489,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   const float s1probe = S1P ? (r + gg) + bl : 0.0f;
   float luma = 0.0f;
   tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
+  H2S_MARK("S2z dark probe");
   // The EOTF table's first segment is marked wherever it is read (S1 on PQ
   // input; the libplacebo branch's IPT decode and curve reads): a value that
   // reached it is huge (> DARK_MARK) in S1's output or the tone map's.  The
@@ -478,28 +507,30 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       if constexpr (LP && TM >= 4 && TM <= 6) probe += luma;   // the NORM curve's decoded intensity
     }
     if (__builtin_amdgcn_ballot_w64(!(probe <= DARK_MARK))) {   // (NaN / inf from a marked value too)
+      H2S_MARK("rare: dark re-run");
       const bool safe2 = to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r, gg, bl);
       tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
     }
   }
+  H2S_MARK("S3 encode");
   if (DBG == 2) dput(r, gg, bl);
   f3 o;
   if (LP && F.lut_off) {
     // LUT off: libplacebo's BT.2020 -> BT.709 matrix on the linear
     // values, the BT.1886 encode clipped to [0, 1] (no rgba rounding: the
     // branch downloads nv12), then Y'CbCr at depth q as below
+    // (255-scaled, into the same folded Y'CbCr rows as the 8-bit codes below)
     auto enc = [&](float x) -> float {
       const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-      return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f) * F.inv255;
+      return __builtin_amdgcn_fmed3f(e, 0.0f, 255.0f);
     };
     const float R = enc(F.m709[0] * r + F.m709[1] * gg + F.m709[2] * bl);
     const float G = enc(F.m709[3] * r + F.m709[4] * gg + F.m709[5] * bl);
     const float B = enc(F.m709[6] * r + F.m709[7] * gg + F.m709[8] * bl);
-    if (DBG == 3 || DBG == 4) dput(R, G, B);
-    const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
-    o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
-    o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
+    if (DBG == 3 || DBG == 4) dput(R * F.inv255, G * F.inv255, B * F.inv255);
+    o.x = fmaf(F.lp_ky[0], R, fmaf(F.lp_ky[1], G, fmaf(F.lp_ky[2], B, K.lp_cy)));
+    o.y = fmaf(F.lp_kcb[0], R, fmaf(F.lp_kcb[1], G, F.lp_kcb[2] * B));
+    o.z = fmaf(F.lp_kcr[0], R, fmaf(F.lp_kcr[1], G, F.lp_kcr[2] * B));
   } else if constexpr (LP) {
     // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the range=tv
     // and rounding / dither offsets, h2s_lp_range / _dither; all >= 0, so the
@@ -510,9 +541,11 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     // lut3d's 8-bit outputs (k_build_lut8x: the generic kernel's own
     // lut3d_8bit arithmetic, bit for bit), instead of a lattice cell, four
     // gathers and the blend per pixel (round 6)
+    // (qoff arrives less lp_k2 lp_qs_f: the encode's - lp_k2 is folded into
+    // the clamp's bounds and the download offset, K.lp_k2 / K.lp_hi)
     auto q8 = [&](float x) -> unsigned {
-      const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
-      return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, 0.0f, 255.0f), F.lp_qs_f, qoff);
+      const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1));
+      return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, K.lp_k2, K.lp_hi), F.lp_qs_f, qoff);
     };
     if (DBG == 3) {
       auto ev = [&](float x) {
@@ -523,23 +556,23 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     }
     unsigned idx;
     const unsigned qr = q8(r), qg = q8(gg), qb = q8(bl);
-    if (F.lp_tab_morton) {   // bit-interleaved (Morton) order: nearby colours share lines
-      asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(spread_lds[qb]), "v"(spread_lds[qg]));
-      asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(idx), "v"(spread_lds[qr]));
-    } else {
-      asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(idx) : "v"(qb), "v"(qg));
-      asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(idx) : "v"(idx), "v"(qr));
-    }
-    const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(lut8x, idx << 2, 0, 0);
-    const float R = (float)(v & 255u) * F.inv255, G = (float)((v >> 8) & 255u) * F.inv255,
-                B = (float)((v >> 16) & 255u) * F.inv255;
-    if (DBG == 4) dput(R, G, B);
-    // BT.709 limited-range Y'CbCr at depth q in the generic kernel's
-    // operation order; o = (luma code + 0.5, 56 q Cb, 56 q Cr)
-    const float Y = F.k709[0] * R + F.k709[1] * G + F.k709[2] * B;
-    o.x = fmaf(16.0f + 219.0f * Y, F.qscale, (EQM ? 0.0f : 0.5f) + ydq);
-    o.y = (F.kcb[0] * R + F.kcb[1] * G + F.kcb[2] * B) * F.c56;
-    o.z = (F.kcr[0] * R + F.kcr[1] * G + F.kcr[2] * B) * F.c56;
+    H2S_MARK("S4 lut3d table read");
+    // the table's bit-interleaved (Morton) index: nearby colours share lines
+    asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(spread_lds[qb]), "v"(spread_lds[qg]));
+    asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(idx), "v"(spread_lds[qr]));
+    // (a global load from a 64-bit VGPR base, one shift-add for the address:
+    // the table's buffer descriptor took four SGPRs that the LP instances
+    // spill, i.e. four lane reads per step)
+    const unsigned v = lut8v[idx];
+    const float R8 = (float)(v & 255u), G8 = (float)((v >> 8) & 255u), B8 = (float)((v >> 16) & 255u);   // (v_cvt_f32_ubyte0..2)
+    H2S_MARK("S5 Y'CbCr");
+    if (DBG == 4) dput(R8 * F.inv255, G8 * F.inv255, B8 * F.inv255);
+    // BT.709 limited-range Y'CbCr at depth q straight from the 8-bit codes
+    // (FastParams lp_ky / lp_kcb / lp_kcr: the rows x 1/255 x the depth
+    // scales, folded on the host); o = (luma code + 0.5, 56 q Cb, 56 q Cr)
+    o.x = fmaf(F.lp_ky[0], R8, fmaf(F.lp_ky[1], G8, fmaf(F.lp_ky[2], B8, K.lp_cy)));
+    o.y = fmaf(F.lp_kcb[0], R8, fmaf(F.lp_kcb[1], G8, F.lp_kcb[2] * B8));
+    o.z = fmaf(F.lp_kcr[0], R8, fmaf(F.lp_kcr[1], G8, F.lp_kcr[2] * B8));
   } else {
     // lattice cell origins (cr, cg, cb) and fractions (dr, dg, db) per channel
     float cr, cg, cb, dr, dg, db;
@@ -654,6 +687,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
            w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
     }
   }
+  H2S_MARK("S7 eq");
   if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
   if constexpr (EQM) {
@@ -725,6 +759,12 @@ template <class T>
 __device__ __forceinline__ T in_vgpr(T x) {
   T y;
   asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
+  return y;
+}
+template <class T>
+__device__ __forceinline__ T* in_vgpr64(T* x) {
+  T* y;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "s"(x));
   return y;
 }
 
@@ -968,7 +1008,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   __shared__ float hrow[2][(CBH + 2) * HST];   // chroma rows (halo incl.) upsampled x2 horizontally
   __shared__ float csum[2][CBH * CBW];         // per chroma sample: sum of its 2x2 pixel contributions
   __shared__ float4 pq_lds[PQ_NSEG + 1];       // [0] = zero segment (pq_z): PQ EOTF, or HLG inverse OETF (!LP)
-  __shared__ float4 pqi_lds[LP ? PQI_NSEG : 1];                   // PQ encode (lp_tone IPT)
+  __shared__ float4 pqi_lds[LP ? PQI_NTAB : 1];                   // PQ encode (lp_tone IPT)
   extern __shared__ uint16_t eq_lds[];         // eq table, codes pre-shifted to the output depth
   __shared__ int tflag[2];                     // per tile parity: some staged code outside the branch-free bound
   __shared__ int offtab[4];                    // +1 corner offsets along r, g, b (H2S_TAGSEL)
@@ -1018,8 +1058,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   }
   __syncthreads();   // the flags are zero before any thread's first commit sets one
   if (LP && F.lp_ipt) {
-    const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NSEG, 0x00020000);
-    for (int i = t; i < PQI_NSEG; i += 256)
+    const __amdgpu_buffer_rsrc_t rpi = __builtin_amdgcn_make_buffer_rsrc((void*)F.pqi_tab, (short)0, 16 * PQI_NTAB, 0x00020000);
+    for (int i = t; i < PQI_NTAB; i += 256)
       pqi_lds[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpi, 16 * i, 0, 0));
   }
 
@@ -1046,37 +1086,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const int og = in_vgpr(F.og), ob = in_vgpr(F.ob), ocr = in_vgpr(F.cr), ocg = in_vgpr(F.cg), ocb = in_vgpr(F.cb);
   const float log2_nm1 = in_vgpr(F.log2_nm1), x_max = in_vgpr(F.x_max);
   const float ysc = in_vgpr(F.ys) * (float)ESC;   // zimg depth-conversion scale
+  // S6 ordered dither (h2s_dither ORDERED, 8-bit quantiser): this lane's
+  // pixel is (xl, yl) mod 8 at every step (tile and step origins are
+  // multiples of 8), so its luma offset is one constant
+  const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
   const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
-                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab};
+                TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab,
+                LP ? in_vgpr(F.lp_k2) : 0.0f, LP ? in_vgpr(F.lp_k2 + 255.0f) : 0.0f, LP ? F.lp_cy + ydq : 0.0f};
+  const unsigned* lut8v = LP ? in_vgpr64(F.lut8x) : nullptr;   // (a 64-bit VGPR base: no SGPRs to spill)
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
   float qo[4];
 #pragma unroll
   for (int i = 0; i < 4; i++)
-    qo[i] = LP ? F.lp_qo + (F.lp_dith ? bayer16(xl + 8 * (i & 1), yl + 8 * (i >> 1)) : 0.5f) : 0.5f;
-  // S6 ordered dither (h2s_dither ORDERED, 8-bit quantiser): this lane's
-  // pixel is (xl, yl) mod 8 at every step (tile and step origins are
-  // multiples of 8), so its luma offset is one constant
-  const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
+    qo[i] = LP ? F.lp_qo + (F.lp_dith ? bayer16(xl + 8 * (i & 1), yl + 8 * (i >> 1)) : 0.5f) -
+                     (F.lut_off ? 0.0f : F.lp_k2 * F.lp_qs_f)
+               : 0.5f;
 
   // the 8 compute steps of one tile; FB (fast body): no pixel of the tile can
   // reach the exact EOTF path and there is no BICUBIC scratch, so the 8 steps
   // are one straight-line block the scheduler can interleave
   auto steps = [&](const TileGeo& g, auto fast) {
     constexpr bool FB = decltype(fast)::value;
+    if constexpr (FB) {
+      H2S_MARK("body: fast");
+    } else {
+      H2S_MARK("body: exact-capable");
+    }
     // BT.2390 / spline: this tile's frame curve (dynamic peak: one record per
     // frame, read through the scalar cache; the frame index is block-uniform)
     CurveConsts cv = F;
     if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
     const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
-    // the libplacebo branch's lut3d 8-bit table (2^24 packed R'G'B' codes, 64 MiB)
-    const __amdgpu_buffer_rsrc_t lut8x = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut8x, (short)0, LP ? (1 << 26) : 0, 0x00020000);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
       const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
       const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
+      H2S_MARK("S0 step: staged Y, vertical chroma");
       const float ybs = ybase[oy];
       const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
       const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
@@ -1086,7 +1134,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
       float oyv, ozv;
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
-          F, cv, pq_lds, pqi_lds, eq_lds, lut8x, spread_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
+          F, cv, pq_lds, pqi_lds, eq_lds, lut8v, spread_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
       if (!FB && F.chr444) {
         // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
         // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
@@ -1096,6 +1144,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
         continue;
       }
       // chroma: 2x2 sums; the 4 lanes of a quad store the same value
+      H2S_MARK("S6 chroma quad sums");
       const float su = quad_sum(oyv), sv = quad_sum(ozv);
       csb[oc] = su;
       csb[oc + CBH * CBW] = sv;
@@ -1108,6 +1157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const int pl = __builtin_amdgcn_readfirstlane(t >> 6) & 1, rem = t & 63;   // chroma store role (t < 128)
   const bool cst = t < 128 && !F.chr444;
   for (;;) {
+    H2S_MARK("tile: commit, prefetch");
     // ---- commit this tile's registers to LDS ----
     if (F.in_mask2 != 0xFFFFFFFFu) {   // h2s_lp_p010 TRUNCATE (block-uniform)
       mask_in(cur.ya), mask_in(cur.ua);
@@ -1131,6 +1181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
       steps(g, std::integral_constant<bool, true>{});
     else
       steps(g, std::integral_constant<bool, false>{});
+    H2S_MARK("tile: store");
     __syncthreads();
 
     // ---- write the tile: 16-byte (u16) / 8-byte (u8) non-temporal stores ----

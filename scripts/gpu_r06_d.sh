@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round 6: the libplacebo instances' VALU cuts (PQ-encode table read, lut3d
+# table through a VGPR base, Y'CbCr rows folded, encode offset folded)
+# against the previous commit's library (scripts/variants/libh2s_lpold.so),
+# same box, alternating; C2 against one more S3 per pixel
+# (profiles/r06/ab_patches/s3_twice.patch, bit-identical); then the GPU suite
+# with the parity report and the default bench.  Stops at the first failure.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=${1:-r06_d}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+NEW=$ROOT/hdr-to-sdr_amd/hdr2sdr/libh2s.so
+OLD=$ROOT/scripts/variants/libh2s_lpold.so
+for i in 1 2; do
+  for v in new old; do
+    lib=$NEW; [ $v = old ] && lib=$OLD
+    timeout -k 10 200 env H2S_LIB=$lib python -u scripts/time_lp_variants_r06.py ${v}_$i >> "$OUT/lp_ab.log" 2>&1 ||
+      { echo "lp $v failed"; tail -5 "$OUT/lp_ab.log"; exit 1; }
+  done
+done
+grep '^{' "$OUT/lp_ab.log"
+rm -f /tmp/ref_hable_*.npy
+KINDS=smooth,website,uniform timeout -k 10 300 python -u scripts/time_variants.py $NEW scripts/variants/libh2s_s3twice.so \
+  $NEW scripts/variants/libh2s_s3twice.so > "$OUT/s3_ab.log" 2>&1 || { echo "s3 ab failed"; tail -5 "$OUT/s3_ab.log"; exit 1; }
+cat "$OUT/s3_ab.log"
+export H2S_FLOAT_REPORT=$OUT/float_report.jsonl
+export H2S_PARITY_REPORT=$OUT/parity_report.jsonl
+rm -f "$H2S_FLOAT_REPORT" "$H2S_PARITY_REPORT"
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=60 -q --timeout 300 --timeout-method thread \
+  > "$OUT/pytest_gpu.log" 2>&1
+rc=$?
+tail -5 "$OUT/pytest_gpu.log"
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "pytest rc=$rc"; exit $rc; }
+timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1 || { echo "bench failed"; tail -5 "$OUT/bench.log"; exit 1; }
+tail -1 "$OUT/bench.log" | cut -c1-600

@@ -25,8 +25,13 @@ def unit_shares(m):
       instructions per CU-cycle, so one per cycle is not.  Every other VALU
       op counts at the full rate (a lower bound: compares, selects,
       conversions, min/max and DPP measured ~1.65x, DESIGN.md §4.1);
-    - valu_active_frac: SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)
-      per SIMD-cycle -- counts waves waiting on their VALU, can pass 1;
+    - valu_waves_per_simd: SQ_ACTIVE_INST_VALU (quad-cycles, counted per
+      wave and summed over waves) per SIMD-cycle: the mean number of a
+      SIMD's waves that have a VALU instruction in flight.  It is an
+      occupancy, not a fraction (two waves overlapping on one SIMD count
+      twice), so it may pass 1; until round 6 it was reported as
+      'valu_active_frac' (VERDICT r05 item 2).  The VALU's utilisation is
+      valu_issue_frac;
     - td_busy_frac / td_tc_stall_frac / ta_busy_frac: the texture data unit
       (L1 -> VGPR return, one per CU) busy, and the share of it waiting for
       the L1; the texture address unit."""
@@ -40,7 +45,7 @@ def unit_shares(m):
         out['valu_issue_frac'] = round((m['SQ_INSTS_VALU'] + m.get('SQ_INSTS_VALU_TRANS_F32', 0.0))
                                        / (cyc * 512), 4)
     if 'SQ_ACTIVE_INST_VALU' in m:
-        out['valu_active_frac'] = round(4 * m['SQ_ACTIVE_INST_VALU'] / (cyc * 1024), 4)
+        out['valu_waves_per_simd'] = round(4 * m['SQ_ACTIVE_INST_VALU'] / (cyc * 1024), 4)
     for key, ctr in (('td_busy_frac', 'TD_TD_BUSY_sum'), ('td_tc_stall_frac', 'TD_TC_STALL_sum'),
                      ('ta_busy_frac', 'TA_TA_BUSY_sum')):
         if ctr in m:
@@ -58,7 +63,8 @@ def from_summary(d):
             m[parts[0]] = float(parts[1])
     path = os.path.join(d, 'traffic.json')
     rec = json.load(open(path))
-    for k in ('valu_issue_frac', 'valu_active_frac', 'td_busy_frac', 'cycles_per_dispatch'):
+    for k in ('valu_issue_frac', 'valu_active_frac', 'valu_waves_per_simd', 'td_busy_frac',
+              'cycles_per_dispatch'):
         rec.pop(k, None)
     rec.update(unit_shares(m))
     with open(path, 'w') as f:

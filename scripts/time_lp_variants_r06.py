@@ -2,7 +2,8 @@
 (C3 BT.2390 IPT, its max(R,G,B) form, spline, libplacebo hable; 16 4K
 frames per call, smooth and uniform content): median ms per call with HIP
 events.  The library is whatever H2S_LIB names (lattice-gather build vs the
-8-bit table) and H2S_LP_TAB picks the table order.  GPU box.
+8-bit table) and H2S_LP_TAB picked the table order (until the linear
+order was removed: profiles/r06/ab_patches/lp_tab_linear.patch).  GPU box.
 Usage: H2S_LIB=... H2S_LP_TAB=0|1 python scripts/time_lp_variants_r06.py TAG"""
 import json
 import os

@@ -34,7 +34,9 @@ def test_unit_shares_formulas():
     # gfx950: a wave64 full-rate op takes 2 cycles of a SIMD-32, a
     # transcendental 4: 2 wave-instructions per CU-cycle is the ceiling
     assert u['valu_issue_frac'] == pytest.approx((0.9 + 0.1) / 2)
-    assert u['valu_active_frac'] == pytest.approx(1.0)
+    # waves with a VALU instruction in flight per SIMD: an occupancy, not a
+    # fraction of the issue rate
+    assert u['valu_waves_per_simd'] == pytest.approx(1.0) and 'valu_active_frac' not in u
     assert (u['td_busy_frac'], u['td_tc_stall_frac'], u['ta_busy_frac']) == pytest.approx((0.93, 0.5, 0.7))
     assert ps.unit_shares({}) == {}
 
