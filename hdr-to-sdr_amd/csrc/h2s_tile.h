@@ -73,6 +73,16 @@ typedef float f3 __attribute__((ext_vector_type(3)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
+// a global pointer held in a VGPR pair (address space 1: the loads through it
+// are global_load, counted in vmcnt only -- a flat load would also count in
+// lgkmcnt, so every LDS wait would wait for it too)
+typedef __attribute__((address_space(1))) const unsigned gu32;
+__device__ __forceinline__ gu32* in_vgpr64(const unsigned* x) {
+  gu32* y;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "s"((gu32*)x));
+  return y;
+}
+
 // streaming frame I/O: non-temporal so the pixels do not evict LUT lines
 __device__ __forceinline__ uint2 nt_ld2(const uint8_t* p) {
   const u2v v = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p));
@@ -447,34 +457,26 @@ struct StepK {
   float nm1;                      // N - 1
   const int* offtab;              // LDS: byte offset of the +1 corner along r, g, b at bytes 0, 4, 8
   float lp_k2, lp_hi, lp_cy;      // LP: the encode's clamp bounds lp_k2, 255 + lp_k2; lp_cy + ydq
+  float lp_k1;                    // LP: the encode's exponent offset (a VGPR: it meets a literal)
 };
 
-// One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
-// y_off, +1 on PQ), x8-upsampled centred chroma U, V -> the eq'd luma code at
-// the output depth (returned) and the pixel's two chroma quantiser
-// contributions (oyv, ozv) for the 2x2 sum.  di: this pixel's index in the
-// debug planes (DBG > 0, frame 0), else -1.
-template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
-__device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
-                                             const float4* pqi_lds, const uint16_t* eq_lds, const unsigned* lut8v, const unsigned* spread_lds,
-                                             __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
-                                             long long di, float& oyv, float& ozv, float qoff, float ydq) {
+// S1 + S2 of one pixel (px_chain, lp_front): staged luma ybs (Y*ys + y_off,
+// +1 on PQ), x8-upsampled centred chroma U, V -> the tone-mapped linear
+// R, G, B, with the dark re-run below.  dput: the debug planes' writer (DBG)
+template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX, class DPut>
+__device__ __forceinline__ void lin_tone(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
+                                         const float4* pqi_lds, const StepK& K, float ybs, float U, float V,
+                                         const DPut& dput, float& r, float& gg, float& bl) {
   // E in table-segment units for the table forms: the PQ EOTF, and the HLG
   // inverse OETF on the CPU chain (the libplacebo branch keeps direct HLG)
   constexpr int ESC = TRC == 0 || !LP ? PQ_SEG : 1;
-  constexpr bool EQM = H2S_EQMAGIC && !LP;   // see the eq lookup at the end
   H2S_MARK("S1a E");
   const float er = fmaf(V, K.a_rv, ybs);
   const float eg = fmaf(V, K.a_gv, fmaf(U, K.a_gu, ybs));
   const float eb = fmaf(U, K.a_bu, ybs);
-  float r, gg, bl;
   H2S_MARK("S1b EOTF");
   const bool safe = to_linear<TRC, ESC, NOEX>(F, pq_lds, er, eg, eb, r, gg, bl);
   H2S_MARK("S2 tone");
-  const long long dpl = (long long)F.dbg_w * F.H;
-  auto dput = [&](float a, float b_, float c) {
-    if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
-  };
   if (DBG == 1) {   // the stage-1 planes with the first segment exact, as the dark re-run below gives them
     float r1, g1, b1;
     to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r1, g1, b1);
@@ -512,6 +514,71 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       tone<TRC, TM, DESAT, LP, true>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe2, emax_s, K.hable_kb, luma);
     }
   }
+}
+
+// The libplacebo branch's rgba8 download and lut3d table read (S3, S4) of one
+// pixel from its tone-mapped linear R, G, B: the BT.1886 encode against the
+// target black, 255 x it rounded to the 8-bit rgba code (qoff: the range=tv
+// and rounding / dither offsets, h2s_lp_range / _dither, less lp_k2 lp_qs_f:
+// the encode's - lp_k2 is folded into the clamp's bounds K.lp_k2 / K.lp_hi;
+// all offsets >= 0, so the conversion's truncation is the floor).
+// Everything after the download -- lut3d's 8-bit coordinate (q / 255)
+// (N-1), the tetrahedral blend in vf_lut3d's order, the truncation to 8 bits
+// -- is a function of the three codes alone, so it is one read of the
+// context's 2^24-entry table of lut3d's 8-bit outputs (k_build_lut8x: the
+// generic kernel's own lut3d_8bit arithmetic, bit for bit), instead of a
+// lattice cell, four gathers and the blend per pixel (round 6, VERDICT r05
+// item 2).  Returns the table entry (R | G << 8 | B << 16) as loaded: the
+// caller decides where to wait for it
+__device__ __forceinline__ unsigned lp_table_read(const FastParams& F, const StepK& K, gu32* lut8v,
+                                                  const unsigned* spread_lds, float r, float gg, float bl,
+                                                  float qoff) {
+  auto q8 = [&](float x) -> unsigned {
+    const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, K.lp_k1));
+    return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, K.lp_k2, K.lp_hi), F.lp_qs_f, qoff);
+  };
+  unsigned idx;
+  const unsigned qr = q8(r), qg = q8(gg), qb = q8(bl);
+  H2S_MARK("S4 lut3d table read");
+  // the table's bit-interleaved (Morton) index: nearby colours share lines
+  asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(spread_lds[qb]), "v"(spread_lds[qg]));
+  asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(idx), "v"(spread_lds[qr]));
+  // (a global load from a 64-bit VGPR base, one shift-add for the address:
+  // the table's buffer descriptor took four SGPRs that the LP instances
+  // spill, i.e. four lane reads per step)
+  return lut8v[idx];
+}
+
+// BT.709 limited-range Y'CbCr at depth q straight from lut3d's 8-bit output
+// codes (FastParams lp_ky / lp_kcb / lp_kcr: the rows x 1/255 x the depth
+// scales, folded on the host): o = (luma code + 0.5, 56 q Cb, 56 q Cr)
+__device__ __forceinline__ f3 lp_ycbcr(const FastParams& F, const StepK& K, float R8, float G8, float B8) {
+  f3 o;
+  o.x = fmaf(F.lp_ky[0], R8, fmaf(F.lp_ky[1], G8, fmaf(F.lp_ky[2], B8, K.lp_cy)));
+  o.y = fmaf(F.lp_kcb[0], R8, fmaf(F.lp_kcb[1], G8, F.lp_kcb[2] * B8));
+  o.z = fmaf(F.lp_kcr[0], R8, fmaf(F.lp_kcr[1], G8, F.lp_kcr[2] * B8));
+  return o;
+}
+
+// One pixel through S1..S7 (both tile kernels): staged luma ybs (Y*ys +
+// y_off, +1 on PQ), x8-upsampled centred chroma U, V -> the eq'd luma code at
+// the output depth (returned) and the pixel's two chroma quantiser
+// contributions (oyv, ozv) for the 2x2 sum.  di: this pixel's index in the
+// debug planes (DBG > 0, frame 0), else -1.  (The libplacebo branch's
+// product steps run lin_tone / lp_table_read / lp_ycbcr software-pipelined
+// instead: k_tile's steps.)
+template <int TRC, int TM, int DESAT, int LP, int DBG, bool NOEX = false>
+__device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveConsts& cv, const float4* pq_lds,
+                                             const float4* pqi_lds, const uint16_t* eq_lds, gu32* lut8v, const unsigned* spread_lds,
+                                             __amdgpu_buffer_rsrc_t lut, const StepK K, float ybs, float U, float V,
+                                             long long di, float& oyv, float& ozv, float qoff, float ydq) {
+  constexpr bool EQM = H2S_EQMAGIC && !LP;   // see the eq lookup at the end
+  const long long dpl = (long long)F.dbg_w * F.H;
+  auto dput = [&](float a, float b_, float c) {
+    if (di >= 0) F.dbg[di] = a, F.dbg[dpl + di] = b_, F.dbg[2 * dpl + di] = c;
+  };
+  float r, gg, bl;
+  lin_tone<TRC, TM, DESAT, LP, DBG, NOEX>(F, cv, pq_lds, pqi_lds, K, ybs, U, V, dput, r, gg, bl);
   H2S_MARK("S3 encode");
   if (DBG == 2) dput(r, gg, bl);
   f3 o;
@@ -532,21 +599,6 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
     o.y = fmaf(F.lp_kcb[0], R, fmaf(F.lp_kcb[1], G, F.lp_kcb[2] * B));
     o.z = fmaf(F.lp_kcr[0], R, fmaf(F.lp_kcr[1], G, F.lp_kcr[2] * B));
   } else if constexpr (LP) {
-    // 255 (BT.1886 encode) rounded to the 8-bit rgba code (qoff: the range=tv
-    // and rounding / dither offsets, h2s_lp_range / _dither; all >= 0, so the
-    // conversion's truncation is the floor).  Everything after the download
-    // -- lut3d's 8-bit coordinate (q / 255) (N-1), the tetrahedral blend in
-    // vf_lut3d's order, the truncation to 8 bits -- is a function of the three
-    // codes alone, so it is one read of the context's 2^24-entry table of
-    // lut3d's 8-bit outputs (k_build_lut8x: the generic kernel's own
-    // lut3d_8bit arithmetic, bit for bit), instead of a lattice cell, four
-    // gathers and the blend per pixel (round 6)
-    // (qoff arrives less lp_k2 lp_qs_f: the encode's - lp_k2 is folded into
-    // the clamp's bounds and the download offset, K.lp_k2 / K.lp_hi)
-    auto q8 = [&](float x) -> unsigned {
-      const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1));
-      return (unsigned)fmaf(__builtin_amdgcn_fmed3f(e, K.lp_k2, K.lp_hi), F.lp_qs_f, qoff);
-    };
     if (DBG == 3) {
       auto ev = [&](float x) {
         const float e = fexp2(fmaf(flog2(__builtin_amdgcn_fmed3f(x, 0.0f, F.lp_xmax)), 1.0f / 2.4f, F.lp_k1)) - F.lp_k2;
@@ -554,25 +606,11 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       };
       dput(ev(r), ev(gg), ev(bl));
     }
-    unsigned idx;
-    const unsigned qr = q8(r), qg = q8(gg), qb = q8(bl);
-    H2S_MARK("S4 lut3d table read");
-    // the table's bit-interleaved (Morton) index: nearby colours share lines
-    asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(spread_lds[qb]), "v"(spread_lds[qg]));
-    asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(idx) : "v"(idx), "v"(spread_lds[qr]));
-    // (a global load from a 64-bit VGPR base, one shift-add for the address:
-    // the table's buffer descriptor took four SGPRs that the LP instances
-    // spill, i.e. four lane reads per step)
-    const unsigned v = lut8v[idx];
+    const unsigned v = lp_table_read(F, K, lut8v, spread_lds, r, gg, bl, qoff);
     const float R8 = (float)(v & 255u), G8 = (float)((v >> 8) & 255u), B8 = (float)((v >> 16) & 255u);   // (v_cvt_f32_ubyte0..2)
     H2S_MARK("S5 Y'CbCr");
     if (DBG == 4) dput(R8 * F.inv255, G8 * F.inv255, B8 * F.inv255);
-    // BT.709 limited-range Y'CbCr at depth q straight from the 8-bit codes
-    // (FastParams lp_ky / lp_kcb / lp_kcr: the rows x 1/255 x the depth
-    // scales, folded on the host); o = (luma code + 0.5, 56 q Cb, 56 q Cr)
-    o.x = fmaf(F.lp_ky[0], R8, fmaf(F.lp_ky[1], G8, fmaf(F.lp_ky[2], B8, K.lp_cy)));
-    o.y = fmaf(F.lp_kcb[0], R8, fmaf(F.lp_kcb[1], G8, F.lp_kcb[2] * B8));
-    o.z = fmaf(F.lp_kcr[0], R8, fmaf(F.lp_kcr[1], G8, F.lp_kcr[2] * B8));
+    o = lp_ycbcr(F, K, R8, G8, B8);
   } else {
     // lattice cell origins (cr, cg, cb) and fractions (dr, dg, db) per channel
     float cr, cg, cb, dr, dg, db;
@@ -759,12 +797,6 @@ template <class T>
 __device__ __forceinline__ T in_vgpr(T x) {
   T y;
   asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
-  return y;
-}
-template <class T>
-__device__ __forceinline__ T* in_vgpr64(T* x) {
-  T* y;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "s"(x));
   return y;
 }
 
@@ -1092,8 +1124,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
   const float ydq = F.dither ? dither_off(xl, yl) - 0.5f : 0.0f;
   const StepK K{a_rv, a_gv, a_gu, a_bu, stride_g, stride_b, og, ob, ocr, ocg, ocb, log2_nm1, x_max,
                 TM == 5 && !LP ? in_vgpr(F.hable_kb) : F.hable_kb, F.c111, rintf(1.0f / F.inv_nm1), offtab,
-                LP ? in_vgpr(F.lp_k2) : 0.0f, LP ? in_vgpr(F.lp_k2 + 255.0f) : 0.0f, LP ? F.lp_cy + ydq : 0.0f};
-  const unsigned* lut8v = LP ? in_vgpr64(F.lut8x) : nullptr;   // (a 64-bit VGPR base: no SGPRs to spill)
+                LP ? in_vgpr(F.lp_k2) : 0.0f, LP ? in_vgpr(F.lp_k2 + 255.0f) : 0.0f, LP ? F.lp_cy + ydq : 0.0f,
+                LP ? in_vgpr(F.lp_k1) : 0.0f};
+  gu32* lut8v = LP ? in_vgpr64(F.lut8x) : nullptr;   // (a 64-bit VGPR base: no SGPRs to spill)
   // libplacebo branch: the rgba8 download offset of this lane's pixel at step
   // s (x mod 16 = xl + 8 (s & 1), y mod 16 = yl + 8 ((s >> 1) & 1): tile
   // origins are multiples of 16)
@@ -1118,12 +1151,79 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
     // frame, read through the scalar cache; the frame index is block-uniform)
     CurveConsts cv = F;
     if ((TM == 7 || TM == 8 || LP) && F.cv_frames) cv = curve_of(F.cv_frames, g.f);
+    if constexpr (LP && TM == 7) {
+      // the curve's constants that meet a second scalar operand in an FMA or
+      // med3 (one scalar operand per VOP3 on gfx950): in VGPRs once per
+      // tile instead of a v_mov per step (libplacebo instances, which have
+      // the VGPRs; round 6)
+      cv.b_e1b = in_vgpr(cv.b_e1b), cv.b_tb = in_vgpr(cv.b_tb), cv.b_c2 = in_vgpr(cv.b_c2);
+      cv.b_lc = in_vgpr(cv.b_lc), cv.b_bk_b = in_vgpr(cv.b_bk_b), cv.b_bk_d = in_vgpr(cv.b_bk_d);
+    } else if constexpr (LP && TM == 8) {
+      cv.sp_qb_u = in_vgpr(cv.sp_qb_u), cv.sp_pb_u = in_vgpr(cv.sp_pb_u);
+      cv.sp_srcmax = in_vgpr(cv.sp_srcmax), cv.sp_umax = in_vgpr(cv.sp_umax);
+    }
     const __amdgpu_buffer_rsrc_t lut = __builtin_amdgcn_make_buffer_rsrc((void*)F.lut_yuv, (short)0, F.lut_bytes, 0x00020000);
+    // the 2x2 chroma sums of step s (or, BICUBIC, the pixel's Cb, Cr into the
+    // frame's 4:4:4 scratch, which k_chroma_bicubic decimates; the scratch
+    // has whole tiles of rows: rows past F.H are written, never read)
+    auto chroma_out = [&](int s, float oyv, float ozv) {
+      if (!FB && F.chr444) {
+        const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
+        F.chr444[(long long)py * F.chr_w + px] = make_float2(oyv * F.inv_c56, ozv * F.inv_c56);
+        return;
+      }
+      // chroma: 2x2 sums; the 4 lanes of a quad store the same value
+      H2S_MARK("S6 chroma quad sums");
+      const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
+      const float su = quad_sum(oyv), sv = quad_sum(ozv);
+      csb[oc] = su;
+      csb[oc + CBH * CBW] = sv;
+    };
+    if constexpr (LP && DBG == 0) {
+      if (!F.lut_off) {   // (launch-uniform)
+        // The libplacebo branch's product steps, software-pipelined: step s's
+        // lut3d table read (a 64 MiB table: its lines come from the L2 or the
+        // MALL) is issued, then step s + 1's S1..S4 run, and only then is
+        // step s finished (Y'CbCr, eq, the luma code into yin, the chroma
+        // sums), so the read's latency hides behind a whole step of VALU work
+        // instead of stalling each step (round 6)
+        unsigned vp = 0;
+#pragma unroll
+        for (int s = 0; s <= 8; s++) {
+          unsigned vn = 0;
+          if (s < 8) {
+            const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);
+            const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
+            H2S_MARK("S0 step: staged Y, vertical chroma");
+            const float ybs = ybase[oy];
+            const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
+            const float V = fmaf(3.0f, h1[oh], h1[oh + hb]);
+            float r, gg, bl;
+            lin_tone<TRC, TM, DESAT, LP, 0, FB>(F, cv, pq_lds, pqi_lds, K, ybs, U, V, [](float, float, float) {},
+                                                 r, gg, bl);
+            H2S_MARK("S3 encode");
+            vn = lp_table_read(F, K, lut8v, spread_lds, r, gg, bl, qo[s & 3]);
+          }
+          if (s > 0) {
+            const int sp = s - 1;
+            const float R8 = (float)(vp & 255u), G8 = (float)((vp >> 8) & 255u), B8 = (float)((vp >> 16) & 255u);
+            H2S_MARK("S5 Y'CbCr");
+            const f3 o = lp_ycbcr(F, K, R8, G8, B8);
+            H2S_MARK("S7 eq");
+            // luma code (eq applied, shifted) replaces the luma sample this lane read
+            reinterpret_cast<unsigned*>(yin)[yl * YST + xl + 8 * (sp >> 1) * YST + 8 * (sp & 1)] = eq_lds[(int)o.x];
+            chroma_out(sp, o.y, o.z);
+          }
+          vp = vn;
+        }
+        return;
+      }
+      H2S_MARK("body: lut off");
+    }
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int oy = 8 * (s >> 1) * YST + 8 * (s & 1);   // compile-time LDS offsets
       const int oh = 4 * (s >> 1) * HST + 8 * (s & 1);
-      const int oc = 4 * (s >> 1) * CBW + 4 * (s & 1);
       H2S_MARK("S0 step: staged Y, vertical chroma");
       const float ybs = ybase[oy];
       const float U = fmaf(3.0f, h0[oh], h0[oh + hb]);   // x8 upsampled, centred, exact
@@ -1135,19 +1235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LP ? H2S_TI
       // luma code (eq applied, shifted) replaces the luma sample this lane read
       reinterpret_cast<unsigned*>(yin)[yl * YST + xl + oy] = px_chain<TRC, TM, DESAT, LP, DBG, FB>(
           F, cv, pq_lds, pqi_lds, eq_lds, lut8v, spread_lds, lut, K, ybs, U, V, di, oyv, ozv, LP ? qo[s & 3] : 0.5f, ydq);
-      if (!FB && F.chr444) {
-        // BICUBIC chroma (h2s_chroma_filter, two-pass): this pixel's Cb, Cr
-        // into the frame's 4:4:4 scratch; k_chroma_bicubic decimates it
-        // (the scratch has whole tiles of rows: rows past F.H are written, never read)
-        const int px = g.px0 + xl + 8 * (s & 1), py = g.py0 + yl + 8 * (s >> 1);
-        F.chr444[(long long)py * F.chr_w + px] = make_float2(oyv * F.inv_c56, ozv * F.inv_c56);
-        continue;
-      }
-      // chroma: 2x2 sums; the 4 lanes of a quad store the same value
-      H2S_MARK("S6 chroma quad sums");
-      const float su = quad_sum(oyv), sv = quad_sum(ozv);
-      csb[oc] = su;
-      csb[oc + CBH * CBW] = sv;
+      chroma_out(s, oyv, ozv);   // (BICUBIC: this pixel's Cb, Cr into the 4:4:4 scratch)
     }
   };
   auto mask_in = [&](uint4& a) {   // h2s_lp_p010 TRUNCATE (block-uniform)

@@ -83,6 +83,24 @@ def main(d):
             if KERNEL in row['Name']:
                 print(f"{row['Name'][:60]}: calls={row['Calls']} avg_ns={float(row['AverageNs']):.0f} "
                       f"min_ns={row['MinNs']} max_ns={row['MaxNs']}")
+    # the warm average: the trace run's dispatches of the kernel after its
+    # warm-up (the bench's --warmup launches, from the trace log's own line)
+    for f in glob.glob(os.path.join(d, 'trace', '**', '*kernel_trace.csv'), recursive=True):
+        dur = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) for r in csv.DictReader(open(f))
+               if KERNEL in r['Kernel_Name']]
+        warm, bench_ms = None, None
+        log = os.path.join(d, 'trace.log')
+        if os.path.exists(log):
+            for line in open(log):
+                if line.startswith('{'):
+                    rec = json.loads(line)
+                    warm, bench_ms = rec.get('warmup'), rec.get('roofline', {}).get('kernel_ms')
+                    step_ms, steps = rec.get('ms_per_step'), rec.get('steps')
+        if dur and warm is not None and len(dur) >= warm + steps:
+            w = dur[warm:warm + steps]   # the timed launches of the headline run
+            print(f'## warm kernel trace: the {len(w)} timed dispatches after {warm} warm-up ones: avg_ns={sum(w) / len(w):.0f} '
+                  f'median_ns={sorted(w)[len(w) // 2]} min_ns={min(w)}; the same run\'s HIP-event kernel_ms '
+                  f'{bench_ms} and ms_per_step {step_ms}')
 
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, 'pmc_*', '**', '*counter_collection.csv'), recursive=True):

@@ -10,10 +10,16 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 ARGS="--steps 6 --warmup 1 --cpu-seconds 0 --no-alt --no-sharded $*"
+# the kernel trace times the bench's own warm loop: 20 untimed launches, then
+# 100 timed ones; prof_summary.py averages the dispatches after the warm-up
+# (the committed trace must compare with ms_per_step)
+TRACE_ARGS="--steps 100 --warmup 20 --cpu-seconds 0 --no-alt --no-sharded $*"
 run() {  # run NAME rocprof-args...
   local name=$1; shift
+  local a=$ARGS
+  [ "$name" = trace ] && a=$TRACE_ARGS
   echo "=== $name"
-  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1
+  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$ROOT/bench.py" $a > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.log"; exit $rc; fi
