@@ -62,8 +62,17 @@
     asm volatile(";@@" name);           \
     __builtin_amdgcn_sched_barrier(0);  \
   } while (0)
+// the same, with three values pinned to the marker (read and rewritten by
+// it), so that the IR passes cannot sink their computation past it
+#define H2S_MARKV(name, a, b, c)                                  \
+  do {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                            \
+    asm volatile(";@@" name : "+v"(a), "+v"(b), "+v"(c));         \
+    __builtin_amdgcn_sched_barrier(0);                            \
+  } while (0)
 #else
 #define H2S_MARK(name)
+#define H2S_MARKV(name, a, b, c)
 #endif
 
 namespace h2s {
@@ -476,7 +485,7 @@ __device__ __forceinline__ void lin_tone(const FastParams& F, const CurveConsts&
   const float eb = fmaf(U, K.a_bu, ybs);
   H2S_MARK("S1b EOTF");
   const bool safe = to_linear<TRC, ESC, NOEX>(F, pq_lds, er, eg, eb, r, gg, bl);
-  H2S_MARK("S2 tone");
+  H2S_MARKV("S2 tone", r, gg, bl);
   if (DBG == 1) {   // the stage-1 planes with the first segment exact, as the dark re-run below gives them
     float r1, g1, b1;
     to_linear<TRC, ESC, NOEX, true>(F, pq_lds, er, eg, eb, r1, g1, b1);
@@ -491,7 +500,7 @@ __device__ __forceinline__ void lin_tone(const FastParams& F, const CurveConsts&
   const float s1probe = S1P ? (r + gg) + bl : 0.0f;
   float luma = 0.0f;
   tone<TRC, TM, DESAT, LP>(F, cv, pq_lds, pqi_lds, r, gg, bl, safe, emax_s, K.hable_kb, luma);
-  H2S_MARK("S2z dark probe");
+  H2S_MARKV("S2z dark probe", r, gg, bl);
   // The EOTF table's first segment is marked wherever it is read (S1 on PQ
   // input; the libplacebo branch's IPT decode and curve reads): a value that
   // reached it is huge (> DARK_MARK) in S1's output or the tone map's.  The
@@ -579,7 +588,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
   };
   float r, gg, bl;
   lin_tone<TRC, TM, DESAT, LP, DBG, NOEX>(F, cv, pq_lds, pqi_lds, K, ybs, U, V, dput, r, gg, bl);
-  H2S_MARK("S3 encode");
+  H2S_MARKV("S3 encode", r, gg, bl);
   if (DBG == 2) dput(r, gg, bl);
   f3 o;
   if (LP && F.lut_off) {
@@ -633,9 +642,11 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       // byte offset truncates to a misaligned record (N = 177: 45 of 3072
       // samples of a uniform frame)
       asm("" : "+v"(sr), "+v"(sg), "+v"(sb));
+      H2S_MARKV("S4a cell, fractions", sr, sg, sb);
       dr = __builtin_amdgcn_fractf(sr), dg = __builtin_amdgcn_fractf(sg), db = __builtin_amdgcn_fractf(sb);
       cr = sr - dr, cg = sg - dg, cb = sb - db;
     }
+    H2S_MARKV("S4b tetrahedron select", dr, dg, db);
     const int base = (int)fmaf(cb, K.stride_b, fmaf(cg, K.stride_g, cr * 12.0f));
     // H2S_TAGSEL (the CPU chain): tetrahedron by sorting axis-tagged
     // fractions: the 4 low mantissa bits of each fraction carry its axis a
@@ -673,6 +684,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
       dmin = __builtin_fminf(__builtin_fminf(dr, dg), db);
       dmid = __builtin_amdgcn_fmed3f(dr, dg, db);
     }
+    H2S_MARKV("S4c weights, uniformity, gathers, blend", dmax, dmid, dmin);
     const float w0 = 1.0f - dmax, w1 = dmax - dmid, w2 = dmid - dmin, w3 = dmin;
     auto blend = [&](const f3 c0, const f3 c1, const f3 c2, const f3 c3) {
       f3 r = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3;
@@ -725,7 +737,7 @@ __device__ __forceinline__ unsigned px_chain(const FastParams& F, const CurveCon
            w0 * q0.z + w1 * q1.z + w2 * q2.z + w3 * q3.z);
     }
   }
-  H2S_MARK("S7 eq");
+  H2S_MARKV("S7 eq", o.x, o.y, o.z);
   if (DBG == 5) dput(o.x - (EQM ? 0.0f : 0.5f) - ydq, 4.0f * o.y, 4.0f * o.z);
   oyv = o.y, ozv = o.z;
   if constexpr (EQM) {

@@ -158,6 +158,8 @@ def table(blocks, skip=(), force=None):
             k = classify(it[1])
             c[k] += 1
             if k == 'valu':
+                c['op:' + it[1].split('_e32')[0].split('_e64')[0]] += 1
+            if k == 'valu':
                 c['slots'] += cost(it[1])
                 if re.match(r'v_(exp|log|rcp|rsq|sqrt|sin|cos)_f32', it[1]):
                     c['trans'] += 1
@@ -179,6 +181,7 @@ def main():
     ap.add_argument('--body', default='fast')
     ap.add_argument('--skip', default='')
     ap.add_argument('--steps', type=int, default=8)
+    ap.add_argument('--ops', default='', help='print the VALU opcode histogram of the stages containing this text')
     a = ap.parse_args()
     blocks = parse(a.listing, a.symbol)
     skip = set(filter(None, a.skip.split(',')))
@@ -205,6 +208,11 @@ def main():
                 tot[k] += c[k] / d
     print(f"| **total (without rare)** | **{tot['valu']:.1f}** | {tot['trans']:.1f} | **{tot['slots']:.1f}** | "
           f"{tot['lds']:.2f} | {tot['vmem']:.2f} | {tot['salu']:.1f} |")
+    if a.ops:
+        for (body, stage), c in rows.items():
+            if a.ops in stage:
+                ops = sorted(((v, k[3:]) for k, v in c.items() if k.startswith('op:')), reverse=True)
+                print(f'\n{stage}: ' + ', '.join(f'{k} {v / a.steps:.2f}' for v, k in ops))
     # joins after the rare re-run and the tile loop's back edge are expected;
     # anything else means a stage boundary the markers do not resolve
     odd = [c for c in conflicts if not any(x[1].startswith(('S', 'rare', 'prologue', 'tile')) for x in c[1:])]
