@@ -4,7 +4,7 @@
 # the sources are copied to a scratch directory, the patch applied there, the
 # product tile instances (h2s_fast.hip, h2s_fast_lp.hip) rebuilt and linked
 # with the in-tree objects of everything else (run the in-tree build first).
-# Usage: bash scripts/build_ablation.sh NAME PATCH
+# Usage: bash scripts/build_ablation.sh NAME PATCH ["-DFLAG ..."]
 # Output: scripts/variants/libh2s_NAME.so (git-ignored, travels with gpurun)
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -19,7 +19,7 @@ cp -r "$ROOT/hdr-to-sdr_amd/csrc" "$T/hdr-to-sdr_amd/"
 cp -r "$ROOT/include" "$T/"
 (cd "$T" && patch -p1 -s < "$PATCH")
 C=$T/hdr-to-sdr_amd/csrc
-FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed -I$T/include"
+FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed -I$T/include ${3:-}"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS -c -o "$T/fast.o" "$C/h2s_fast.hip" &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS -c -o "$T/fastlp.o" "$C/h2s_fast_lp.hip" &
 wait %1 && wait %2
