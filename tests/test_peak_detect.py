@@ -340,3 +340,34 @@ def test_gpu_preview_restores_the_contexts_peak_state():
     b = tm(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:]), W, H, 10)).buf
     tm.close()
     assert np.array_equal(np.concatenate([a, b]), want)
+
+
+@pytest.mark.gpu
+def test_gpu_preview_restores_the_peak_state_when_it_fails():
+    """a preview whose per-frame conversion fails after its
+    launch (the H2S_OPT_TEST_FAIL_AFTER_LAUNCH hook) still restores the
+    context's own peak state before returning the error, so the sequence
+    continues as if no preview had run."""
+    import ctypes
+    from hdr2sdr import _abi
+    from test_gpu_parity import lattice
+    W, H = 256, 128
+    buf = sequence(W, H)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, bits_out=8, maxcll=4000.0)
+    seq = hdr2sdr.Tonemapper(0, params, lattice(65))
+    want = seq(hdr2sdr.FrameBatch(np.ascontiguousarray(buf), W, H, 10)).buf
+    seq.close()
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    a = tm(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[:3]), W, H, 10)).buf
+    before = tm.peak_state()
+    rgb = np.empty((2, H, W, 3), np.uint8)
+    d = hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:5]), W, H, 10).descriptor()
+    L = _abi.lib()
+    tm.set_option(_abi.OPT_TEST_FAIL_AFTER_LAUNCH, 1)
+    rc = L.h2s_preview_rgb24_batch(tm._ctx, ctypes.byref(d), 2, rgb.ctypes.data, 3 * W, 3 * W * H, W, H, 1.0,
+                                   _abi.LOC_HOST, None)
+    assert rc == _abi.H2S_E_HIP and b'injected failure' in L.h2s_last_error(tm._ctx)
+    assert tm.peak_state() == before
+    b = tm(hdr2sdr.FrameBatch(np.ascontiguousarray(buf[3:]), W, H, 10)).buf
+    tm.close()
+    assert np.array_equal(np.concatenate([a, b]), want)
