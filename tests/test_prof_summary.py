@@ -41,11 +41,11 @@ def test_unit_shares_formulas():
     assert ps.unit_shares({}) == {}
 
 
-@pytest.mark.parametrize('sub', ['prof', 'prof_c3'])
+@pytest.mark.parametrize('sub', ['r05/closing/prof', 'r05/closing/prof_c3', 'r06/closing/prof_c2', 'r06/closing/prof_c3'])
 def test_closing_profiles_rederive_from_their_summaries(tmp_path, sub):
-    """profiles/r05/closing/<sub>/traffic.json holds what its summary.txt's
-    counter means give (the raw per-dispatch CSVs are not kept)."""
-    src = os.path.join(REPO, 'profiles', 'r05', 'closing', sub)
+    """profiles/<round>/closing/<sub>/traffic.json holds what its
+    summary.txt's counter means give (the raw per-dispatch CSVs are not kept)."""
+    src = os.path.join(REPO, 'profiles', *sub.split('/'))
     for f in ('summary.txt', 'traffic.json'):
         shutil.copy(os.path.join(src, f), tmp_path / f)
     ps.from_summary(str(tmp_path))
@@ -56,9 +56,11 @@ def test_closing_profiles_rederive_from_their_summaries(tmp_path, sub):
 
 
 def test_bench_reads_the_c2_traffic_of_its_own_workload():
+    """The newest round's profile of the bench's own workload wins
+    (profiles/r06/traffic.json: the round-6 closing profile of C2)."""
     bench = _load('bench_mod', os.path.join(REPO, 'bench.py'))
-    c2 = json.load(open(os.path.join(REPO, 'profiles', 'r05', 'traffic.json')))
+    c2 = json.load(open(os.path.join(REPO, 'profiles', 'r06', 'traffic.json')))
     tr = bench.pmc_traffic(c2['workload'])
-    assert tr is not None and tr['source'].startswith('profiles/r05/traffic.json')
+    assert tr is not None and tr['source'].startswith('profiles/r06/traffic.json')
     assert tr['bytes_per_dispatch'] == c2['bytes_per_dispatch']
     assert bench.pmc_traffic(c2['workload'].replace('64 frames', '16 frames')) is None
