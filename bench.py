@@ -380,10 +380,20 @@ def main():
                 ('C3_spline', dict(tonemapper='spline', gamma=1.0, bits_out=10), 3840, 2160, 16, 65),
                 # C3 with libplacebo's peak_detect=1 (src/utils.py:448): statistics + finish (device IIR, curve records), one tile launch
                 ('C3_dyn', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=True, maxcll=4000.0),
-                 3840, 2160, 16, 65)):
+                 3840, 2160, 16, 65),
+                # C3 on the reference's own website frame (real content: its colours
+                # cluster, so the lut3d table's lines mostly stay in the L2)
+                ('C3_website', dict(tonemapper='bt.2390', gamma=1.0, bits_out=10), 3840, 2160, 16, 65)):
+            if tag.endswith('_website') and not os.path.exists(real_npz):
+                continue
             p_ = hdr2sdr.TonemapParams(mode=args.mode, **kw)
             t_ = hdr2sdr.Tonemapper(local, p_, hdr2sdr.generate_lattice(lut_n))
-            src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)
+            if tag.endswith('_website'):
+                import numpy as np
+                from hdr2sdr.synth import frames_from_rgb8
+                src_ = frames_from_rgb8(np.load(real_npz)['hdr'], nf, p_.bits_in, dev)
+            else:
+                src_ = synth_frames('smooth', nf, w_, h_, p_.bits_in, device=dev, seed=0x5EED)
             dst_ = hdr2sdr.FrameBatch.empty_torch(nf, w_, h_, p_.bits_out, dev)
             st_ = torch.cuda.current_stream(dev)
 
@@ -400,6 +410,7 @@ def main():
             kms_ = timed_(t_)
             b_ = 1.5 * (1 if p_.bits_in == 8 else 2) + 1.5 * (1 if p_.bits_out == 8 else 2)
             other[tag] = {'size': f'{w_}x{h_}', 'frames': nf, 'tonemapper': kw['tonemapper'], 'lut': lut_n,
+                          'content': 'website frame' if tag.endswith('_website') else 'smooth',
                           'bits': f"{p_.bits_in}->{p_.bits_out}", 'kernel_ms': round(kms_, 4),
                           'mpx_s': round(nf * w_ * h_ / kms_ / 1e3, 1),
                           'hbm_frac': round(b_ * nf * w_ * h_ / (kms_ / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}

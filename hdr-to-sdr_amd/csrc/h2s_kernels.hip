@@ -10,6 +10,8 @@
 // contiguous range of rows (chroma halo rows and LUT lines stay in its L2).
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "h2s_device.h"
 #include "h2s_lpx.h"
 #include "h2s_peak.h"
@@ -925,5 +927,30 @@ extern "C" __attribute__((visibility("default"))) int h2stest_libm(int fn, const
   }
   if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, b, hipMemcpyDeviceToHost);
   hipFree(d);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+// private test hook (not in include/h2s.h): the libplacebo branch's lut3d
+// 8-bit table (k_build_lut8x) for a host lattice of n^3 R'G'B' records (3
+// floats each, r fastest), copied back in the kernel's bit-interleaved
+// order (2^24 u32).  For tests/test_gpu_parity.py's whole-table comparison
+// with the oracle's lut3d 8-bit path.  Returns 0 or a negative HIP error.
+extern "C" __attribute__((visibility("default"))) int h2stest_lut8x(const float* lut_rgb, int n, unsigned* out) {
+  if (n < 2 || n > 256) return -1;
+  const size_t nn = (size_t)n * n * n;
+  std::vector<float4> l4(nn + 1, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  for (size_t i = 0; i < nn; i++) l4[i] = make_float4(lut_rgb[3 * i], lut_rgb[3 * i + 1], lut_rgb[3 * i + 2], 0.0f);
+  float4* dl = nullptr;
+  unsigned* dt = nullptr;
+  if (hipMalloc(&dl, l4.size() * sizeof(float4)) != hipSuccess) return -1;
+  if (hipMalloc(&dt, sizeof(unsigned) << 24) != hipSuccess) {
+    hipFree(dl);
+    return -1;
+  }
+  hipError_t e = hipMemcpy(dl, l4.data(), l4.size() * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = h2s::build_lut8x(dl, n, dt, 0);
+  if (e == hipSuccess) e = hipMemcpy(out, dt, sizeof(unsigned) << 24, hipMemcpyDeviceToHost);
+  hipFree(dl);
+  hipFree(dt);
   return e == hipSuccess ? 0 : -(int)e;
 }

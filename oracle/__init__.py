@@ -217,6 +217,21 @@ def tonemap_lin(params: Params, lattice: 'np.ndarray | None', rgb: np.ndarray, a
     return out.reshape(shp)
 
 
+def lut8x_table(lattice: np.ndarray) -> np.ndarray:
+    """lut3d's 8-bit path (oracle lut3d_8bit) for every rgba8 code triple:
+    2^24 uint32, R | G << 8 | B << 16 at index r | g << 8 | b << 16."""
+    lat = np.ascontiguousarray(lattice, dtype=np.float32).reshape(-1, 3)
+    n = round(lat.shape[0] ** (1 / 3))
+    out = np.empty(1 << 24, dtype=np.uint32)
+    L = lib()
+    L.oracle_lut8x_table.restype = ctypes.c_int
+    L.oracle_lut8x_table.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    rc = L.oracle_lut8x_table(lat.ctypes.data, n, out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_lut8x_table failed: {rc}')
+    return out
+
+
 def lp_download(params: Params, lattice: np.ndarray, buf: np.ndarray, width: int, height: int,
                 avg_pq: float = 0.0) -> np.ndarray:
     """libplacebo branch with the LUT: the exact (double) pre-rounding value x

@@ -1441,6 +1441,26 @@ static void o_resize(const uint8_t *src, int sw, int sh, uint8_t *dst, int ow, i
 }
 
 /* yuv8: one tight yuv420p frame (W x H) as the chain produced it */
+/* lut3d's 8-bit path for every rgba8 code triple, packed R | G << 8 |
+ * B << 16 at index r | g << 8 | b << 16 (tests: the tile kernel's table,
+ * k_build_lut8x, against lut3d_8bit above, all 2^24 entries) */
+int oracle_lut8x_table(const float *lut, int lut_n, uint32_t *out) {
+  ocfg c;
+  memset(&c, 0, sizeof c);
+  c.lut = lut, c.lut_n = lut_n;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (int b = 0; b < 256; b++)
+    for (int g = 0; g < 256; g++)
+      for (int r = 0; r < 256; r++) {
+        const rgbf q = lut3d_8bit(&c, r, g, b);
+        out[((size_t)b << 16) | ((size_t)g << 8) | (size_t)r] =
+            (uint32_t)q.r | ((uint32_t)q.g << 8) | ((uint32_t)q.b << 16);
+      }
+  return 0;
+}
+
 int oracle_preview_tail(const uint8_t *yuv8, int W, int H, int ow, int oh, double gamma, uint8_t *rgb) {
   const int cw = W / 2, ch = H / 2, ow2 = (ow + 1) / 2, oh2 = (oh + 1) / 2;
   const uint8_t *Y = yuv8, *U = yuv8 + (size_t)W * H, *V = U + (size_t)cw * ch;

@@ -255,6 +255,37 @@ def test_lut_sizes_libplacebo(tm, lut_n):
     assert tm.query_path(src, dst) == _abi.PATH_TILE
 
 
+def _morton_to_linear():
+    """For each index of the tile kernel's bit-interleaved table, the linear
+    index r | g << 8 | b << 16 of its code triple."""
+    i = np.arange(1 << 24, dtype=np.uint32)
+    r = np.zeros_like(i)
+    g = np.zeros_like(i)
+    b = np.zeros_like(i)
+    for k in range(8):
+        r |= ((i >> (3 * k)) & 1) << k
+        g |= ((i >> (3 * k + 1)) & 1) << k
+        b |= ((i >> (3 * k + 2)) & 1) << k
+    return r | (g << 8) | (b << 16)
+
+
+@pytest.mark.parametrize('lut_n', [2, 33, 65, 177, 256])
+def test_lut8x_table_equals_the_oracle_lut3d_8bit(lut_n):
+    """The libplacebo branch's lut3d table (k_build_lut8x, through the
+    private entry h2stest_lut8x) equals the oracle's lut3d 8-bit path for
+    every one of the 2^24 rgba8 code triples, bit for bit."""
+    from hdr2sdr import _abi
+    L = ctypes.CDLL(_abi.LIB_PATH)
+    L.h2stest_lut8x.restype = ctypes.c_int
+    L.h2stest_lut8x.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lat = np.ascontiguousarray(lattice(lut_n), dtype=np.float32)
+    got = np.empty(1 << 24, dtype=np.uint32)
+    assert L.h2stest_lut8x(lat.ctypes.data, lut_n, got.ctypes.data) == 0
+    want = oracle.lut8x_table(lat)[_morton_to_linear()]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad.size, [(int(i), hex(int(got[i])), hex(int(want[i]))) for i in bad[:5]])
+
+
 def test_lut8x_table_rebuilt_after_set_lut(tm):
     """The 8-bit table follows the lattice: a new h2s_set_lut (another size,
     then the first again) changes the branch's output as the oracle's."""

@@ -80,3 +80,26 @@ def test_download_values_round_to_the_oracle_codes():
     s3 = oracle.debug_float(op, lattice(65), src, W, H, 3).astype(np.float64)
     assert np.all(np.abs(np.clip(s3, 0, 1) * 255 + 0.5 - x) < 1e-4)
     assert np.isfinite(x).all()
+
+
+def test_oracle_lut8x_table_is_lut3d_8bit():
+    """oracle.lut8x_table (the reference the GPU suite compares the tile
+    kernel's whole table with): the lattice nodes come back truncated to 8
+    bits where the code lands exactly on a node (q = 0 and q = 255), and the
+    table agrees with the oracle chain's own lut3d stage (the stage-4 plane of
+    the debug output) on a frame's download codes."""
+    lat = lattice(65)
+    tab = oracle.lut8x_table(lat)
+    l = np.asarray(lat, np.float32).reshape(-1, 3)
+    for code, node in ((0, 0), (255, 65 ** 3 - 1)):
+        want = np.minimum(np.maximum((l[node] * np.float32(255.0)).astype(np.int64), 0), 255)
+        got = int(tab[code | code << 8 | code << 16])
+        assert [got & 255, (got >> 8) & 255, got >> 16] == list(want)
+    p = hdr2sdr.TonemapParams(tonemapper='bt.2390', bits_out=10)
+    op = oracle.params_from(p.to_c())
+    src = synth_frames('smooth', 1, W, H, 10, device='cpu', seed=3).to_numpy().buf
+    q = np.floor(oracle.lp_download(op, lat, src, W, H)).astype(np.int64)        # [3, H, W] rgba8 codes
+    s4 = oracle.debug_float(op, lat, src, W, H, 4).astype(np.float64)           # lut3d's 8-bit output / 255
+    e = tab[(q[0] | q[1] << 8 | q[2] << 16).ravel()]
+    got = np.stack([e & 255, (e >> 8) & 255, e >> 16]).reshape(3, H, W).astype(np.float64)
+    assert np.array_equal(got, np.rint(s4.reshape(3, H, W) * 255.0))
