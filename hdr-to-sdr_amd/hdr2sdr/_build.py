@@ -79,6 +79,18 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
         except OSError:
             return True
 
+    # the gpurun snapshot carries libh2s.so but not build/obj: a library newer
+    # than every source and header, linked from objects built with today's
+    # flags (its .cmd stamp), is current without its objects
+    stamp = '\n'.join(f'{os.path.basename(s)}: ' + ' '.join(flags(s)) for s in srcs)
+    try:
+        with open(LIB + '.cmd') as fh:
+            lib_cmd = fh.read()
+    except OSError:
+        lib_cmd = None
+    if not force and lib_cmd == stamp and not _stale(LIB, srcs + hdrs):
+        return LIB
+
     todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s] + hdrs) or cmd_stale(s, o)]
 
     def compile_one(so):
@@ -94,14 +106,15 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), int(os.environ.get('MAX_JOBS', '8'))))) as ex:
         list(ex.map(compile_one, todo))
-    if not force and not todo and not _stale(LIB, objs):
-        return LIB
-    tmp = LIB + f'.tmp{os.getpid()}'
-    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', tmp] + objs
-    if verbose:
-        print(' '.join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    if force or todo or _stale(LIB, objs):
+        tmp = LIB + f'.tmp{os.getpid()}'
+        cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', tmp] + objs
+        if verbose:
+            print(' '.join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, LIB)
+    with open(LIB + '.cmd', 'w') as fh:
+        fh.write(stamp)
     return LIB
 
 
