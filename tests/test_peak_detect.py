@@ -195,6 +195,40 @@ def test_gpu_dynamic_peak_with_switches_matches_oracle(kw):
     assert_close_int(params, dst.buf.astype(np.int64), want.astype(np.int64), W, H, buf, knees=knees)
 
 
+def _saturated_frames(W, H):
+    """Frames with pixels at E > 1 (Y' code 1023: PQ(max R,G,B) clamps to 1
+    exactly, the histogram's top edge): a band of whole rows (statistics units
+    inside one bin) and every fifth column (units spanning bins), each beside
+    E = 0.5."""
+    a = _flat_frame(64 + round(0.5 * 876), W=W, H=H)
+    a.y[0, : H // 5, :] = 1023
+    b = _flat_frame(64 + round(0.5 * 876), W=W, H=H)
+    b.y[0, :, ::5] = 1023
+    return np.concatenate([a.buf, b.buf])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('pct', [float('nan'), 90.0, 100.0])   # nan: vf_libplacebo's 99.995
+@pytest.mark.parametrize('W,H', [(256, 128), (200, 96)])       # quad form; row / generic form
+def test_gpu_peak_stats_equal_the_oracle(W, H, pct):
+    """h2s_peak_stats (the per-frame percentile measurement and mean) against
+    the oracle's, on the sequence and on frames with saturated pixels, whose
+    PQ value 1 sits on the histogram's top edge."""
+    import torch
+    from test_gpu_parity import lattice
+    buf = np.concatenate([sequence(W, H), _saturated_frames(W, H)])
+    kw = {} if math.isnan(pct) else dict(pd_percentile=pct)
+    params = hdr2sdr.TonemapParams(tonemapper='bt.2390', peak_detect=True, maxcll=4000.0, **kw)
+    tm = hdr2sdr.Tonemapper(0, params, lattice(65))
+    fmax, favg = tm.peak_stats(hdr2sdr.FrameBatch(torch.from_numpy(buf).cuda(), W, H, 10))
+    tm.close()
+    mx, avg = oracle.peak_stats(oracle.params_from(params.to_c()), buf, W, H)
+    np.testing.assert_allclose(fmax, mx, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(favg, avg, rtol=1e-5, atol=1e-6)
+    if pct == 90.0:          # a fifth of the pixels saturate: the 90th percentile is in the top bin
+        assert (fmax[-2:] > 1023 / 1024).all()
+
+
 @pytest.mark.gpu
 def test_gpu_peak_reset_restarts_the_sequence():
     from test_gpu_parity import lattice
