@@ -1,6 +1,6 @@
 """The dynamic-peak statistics kernel alone, for a kernel trace of a library
 variant (H2S_LIB, scripts/build_ablation.sh): h2s_peak_stats over 16 4K
-frames of the bench content (or argv[1]: a synth kind, or website), REPS times with the percentile histogram and
+frames of the bench content (or argv[1]: a synth kind, or website; argv[2]: blocks per frame), REPS times with the percentile histogram and
 REPS times without (pd_percentile 100).  GPU box.
 Usage: H2S_LIB=... rocprofv3 --kernel-trace ... -- python3 scripts/bench_peak_kernel.py"""
 import os
@@ -26,6 +26,9 @@ for pct in (float('nan'), 100.0):
     p = hdr2sdr.TonemapParams(tonemapper='bt.2390', gamma=1.0, bits_out=10, peak_detect=True, maxcll=4000.0,
                               pd_percentile=pct)
     tm = hdr2sdr.Tonemapper(0, p, lat)
+    if len(sys.argv) > 2:   # partial records (blocks) per frame
+        from hdr2sdr import _abi
+        tm.set_option(_abi.OPT_TEST_PEAK_BLOCKS, int(sys.argv[2]))
     for _ in range(REPS):
         tm.peak_stats(src)
     torch.cuda.synchronize()
