@@ -6,12 +6,13 @@
 # other translation unit the patch touches, or all of them when it touches a
 # header -- and linked with the in-tree objects of everything else (run the
 # in-tree build first).
-# Usage: bash scripts/build_ablation.sh NAME PATCH ["-DFLAG ..."]
+# Usage: bash scripts/build_ablation.sh NAME PATCH|none ["-DFLAG ..."]
 # Output: scripts/variants/libh2s_NAME.so (git-ignored, travels with gpurun)
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1
-PATCH=$(cd "$(dirname "$2")" && pwd)/$(basename "$2")
+PATCH=/dev/null   # "none": the product source, built with FLAGS only
+if [ "$2" != none ]; then PATCH=$(cd "$(dirname "$2")" && pwd)/$(basename "$2"); fi
 O=$ROOT/hdr-to-sdr_amd/build/obj
 V=$ROOT/scripts/variants
 T=$(mktemp -d /tmp/h2s_abl_XXXX)
@@ -19,7 +20,7 @@ trap 'rm -rf "$T"' EXIT
 mkdir -p "$V" "$T/hdr-to-sdr_amd"
 cp -r "$ROOT/hdr-to-sdr_amd/csrc" "$T/hdr-to-sdr_amd/"
 cp -r "$ROOT/include" "$T/"
-(cd "$T" && patch -p1 -s < "$PATCH")
+if [ "$PATCH" != /dev/null ]; then (cd "$T" && patch -p1 -s < "$PATCH"); fi
 C=$T/hdr-to-sdr_amd/csrc
 FLAGS="-O3 -std=c++17 -fno-slp-vectorize -fPIC -Wno-unused-value -Wno-unused-result -Wno-pass-failed -I$T/include ${3:-}"
 HDR=0
